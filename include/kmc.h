@@ -1,0 +1,166 @@
+/* kmc.h — C-ABI of libkmc, the MI355X (gfx950) engine for the per-timestep
+ * KMC diffusion–reaction loop of xiaopuren/KMC-with-a-diffusion-reaction-
+ * algorithm.
+ *
+ * The reference has no plugin/FFI surface: its "interface"
+ * is the set of global arrays main() mutates (main.cpp:102-168) and the
+ * process/file contract (position.cpt in, bond.dat/position.cpt out,
+ * main.cpp:226-270, 2206-2253).  This header is the drop-in boundary a host
+ * program binds instead: plain pointers and sizes, no torch types, int return
+ * codes (0 = ok, < 0 = error; kmc_last_error() has the message).  One handle
+ * per GPU; a handle is used by one host thread at a time.
+ *
+ * Indices inside state buffers follow the reference exactly: proteins are
+ * 1-based, receptors ("protein_A") are 1..n_a, ligands ("protein_B") are
+ * n_a+1..n_a+n_b, and 0 means "no neighbour" (main.cpp:117, 1926-1928).
+ */
+#ifndef KMC_H
+#define KMC_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KMC_OK 0
+#define KMC_ERR_ARG (-1)       /* bad argument / size mismatch */
+#define KMC_ERR_IO (-2)        /* file could not be opened or written */
+#define KMC_ERR_FORMAT (-3)    /* malformed position.cpt */
+#define KMC_ERR_STATE (-4)     /* bond links inconsistent (status vs res_nei) */
+#define KMC_ERR_PLACEMENT (-5) /* random placement exhausted its attempts */
+#define KMC_ERR_CAPACITY (-6)  /* a fixed device capacity was exceeded */
+#define KMC_ERR_HIP (-7)       /* HIP runtime error */
+#define KMC_ERR_GEOMETRY (-8)  /* a rigid body left the cell-list extent bound */
+#define KMC_ERR_NODEVICE (-9)  /* no gfx950 device / kernels not loaded */
+
+/* Physics + run parameters.  Defaults (kmc_params_default) equal the
+ * reference globals at main.cpp:39-99. */
+typedef struct kmc_params {
+  int32_t n_a;               /* protein_A_tot_num (main.cpp:48) */
+  int32_t n_b;               /* protein_B_tot_num (main.cpp:57) */
+  double time_step;          /* ns (main.cpp:40) */
+  double box_x, box_y, box_z;/* cell_range_x/y/z (main.cpp:43-45) */
+  double pai;                /* 3.1415926 (main.cpp:71) */
+  double ra_radius, ra_D, ra_rot_D;      /* main.cpp:72-74 */
+  double rb_radius, rb_D, rb_rot_D;      /* main.cpp:76-78 */
+  double mono_cis_ass_rate, mono_cis_diss_rate;           /* main.cpp:80-81 */
+  double cis_D, cis_rot_D, cis_ass_rate, cis_diss_rate;   /* main.cpp:83-86 */
+  double bond_D, bond_rot_D, ass_rate, diss_rate;         /* main.cpp:88-91 */
+  double bond_dist_cutoff;   /* 18  (main.cpp:93) */
+  double bond_thetapd_cutoff;/* 45  (main.cpp:95) */
+  double bond_thetaot_cutoff;/* 90  (main.cpp:97) */
+  double cis_thetaot_cutoff; /* 10  (main.cpp:98) */
+  double cis_dist_cutoff;    /* 15  (main.cpp:99) */
+  int64_t simu_step;         /* last step of a full run (main.cpp:39) */
+  int32_t out_interval;      /* checkpoint / bond.dat cadence, 5000 (main.cpp:2206) */
+  int32_t reserved0;
+  uint64_t seed;             /* Philox key (replaces the clock seed of rand2) */
+  uint32_t replica;          /* independent trajectory id (ensembles) */
+  int32_t reserved1;
+} kmc_params;
+
+/* One record per simulated step: the bond.dat columns (main.cpp:2251) plus
+ * the raw cluster sums they come from. */
+typedef struct kmc_obs {
+  int64_t step;                 /* mc_time_step */
+  double t;                     /* mc_time_step * time_step */
+  int32_t bond_num_rl;
+  int32_t bond_num_mono_cis;
+  int32_t bond_num_cis;
+  int32_t bond_num;
+  double cluster_size;          /* tot_proteins_in_cluster / tot_cluster_num */
+  int32_t protein_num_in_max_complex;
+  int32_t tot_proteins_in_cluster;
+  int32_t tot_cluster_num;
+  int32_t reserved;
+} kmc_obs;
+
+/* Host-side state buffers (caller-owned), structure-of-arrays, fp64.
+ *   ra  : 48 * n_a doubles, ra[(((j-1)*4 + (k-1))*3 + c) * n_a + (i-1)]
+ *         = R_{x,y,z}[i][j][k] of receptor i (j,k = 1..4; c = 0,1,2 → x,y,z)
+ *   rb  : 24 * n_b doubles, rb[(((j-1)*2 + (k-1))*3 + c) * n_b + (b-1)]
+ *         = R_{x,y,z}[n_a+b][j][k] of ligand b (j = 1..4, k = 1..2)
+ *   a_int: 5 * n_a int32 in checkpoint order: protein_status[i][2],
+ *         protein_status[i][3], res_nei[i][2], res_nei[i][4], res_nei[i][3]
+ *         (a_int[f * n_a + (i-1)], main.cpp:240-244)
+ *   b_int: 8 * n_b int32: protein_status[.][1..4] then res_nei[.][1..4]
+ *   counters: bond_num, bond_num_rl, bond_num_cis, bond_num_mono_cis,
+ *         protein_num_in_Max_Complex (main.cpp:261-265)
+ *   step: the last completed mc_time_step (0 for a fresh configuration). */
+typedef struct kmc_state_view {
+  double* ra;
+  double* rb;
+  int32_t* a_int;
+  int32_t* b_int;
+  int32_t counters[5];
+  int32_t reserved;
+  int64_t step;
+} kmc_state_view;
+
+typedef struct kmc_sim kmc_sim;
+
+/* Reference defaults (main.cpp:39-99); out_interval 5000, seed 1, replica 0. */
+void kmc_params_default(kmc_params* p);
+
+/* Create a simulation on HIP device `device` (-1 = current). */
+int kmc_create(const kmc_params* p, int device, kmc_sim** out);
+int kmc_destroy(kmc_sim* s);
+const char* kmc_last_error(const kmc_sim* s);
+
+/* Random initial configuration with the reference's placement rules
+ * (main.cpp:281-447: rejection of overlapping receptors / ligands, random
+ * orientations), drawn from the keyed RNG; O(N) with a hash grid, so it also
+ * serves the 1e6–1e7-particle configurations the reference's O(N^2) goto
+ * sampler cannot reach.  Resets counters and sets step = 0. */
+int kmc_init_random(kmc_sim* s);
+
+/* position.cpt reader / writer, byte-compatible with main.cpp:226-270 and
+ * main.cpp:2206-2244.  After a load the next simulated step is saved+1
+ * (main.cpp:267). */
+int kmc_load_cpt(kmc_sim* s, const char* path);
+int kmc_write_cpt(kmc_sim* s, const char* path);
+
+/* Copy the state in / out of the device (host buffers sized as above). */
+int kmc_set_state(kmc_sim* s, const kmc_state_view* v);
+int kmc_get_state(kmc_sim* s, kmc_state_view* v);
+
+/* Advance nsteps time steps of the diffusion–reaction loop (main.cpp:461-2308)
+ * on the GPU.  `out` (may be NULL) receives nsteps records. */
+int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out);
+
+/* Last completed step number. */
+int64_t kmc_current_step(const kmc_sim* s);
+
+/* Device time of the most recent kmc_step call's per-phase kernels, for the
+ * benchmark's roofline accounting (ms, summed over the call). */
+int kmc_phase_times(const kmc_sim* s, double* ms_out, int32_t n);
+
+/* Formatting helpers shared by every host driver.  Each returns the number of
+ * characters written (excluding NUL) or < 0. */
+int kmc_format_bond_line(const kmc_params* p, const kmc_obs* o, char* buf, size_t n);   /* main.cpp:2251 */
+
+/* FNV-1a-64 hash of a host state view in reference order (beads x,y,z as
+ * IEEE bits, then the ints, then counters and step): the per-step parity
+ * fingerprint shared by the oracle, the reference trace and the GPU tests. */
+uint64_t kmc_state_hash(const kmc_params* p, const kmc_state_view* v);
+
+/* Host-only helpers (no device needed): the same formats and generator as
+ * above on caller-owned host buffers. */
+const char* kmc_host_last_error(void);
+int kmc_host_load_cpt(const kmc_params* p, const char* path, kmc_state_view* v);
+int kmc_host_write_cpt(const kmc_params* p, const kmc_state_view* v, const char* path);
+int kmc_host_init_random(const kmc_params* p, kmc_state_view* v);
+/* bond-link consistency + rigid-body extent bound; KMC_OK or an error code */
+int kmc_host_validate(const kmc_params* p, const kmc_state_view* v);
+
+/* Diagnostics: the portable math of kmc_math.h evaluated on the host and on
+ * the device (op 0 sin, 1 cos, 2 atan2(x,y), 3 acos, 4 sqrt, 5 x/y, 6 round)
+ * — the GPU numerics test compares the two bit for bit. */
+int kmc_host_math(int op, const double* x, const double* y, double* out, int64_t n);
+int kmc_device_math(int op, const double* x, const double* y, double* out, int64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KMC_H */

@@ -1,0 +1,151 @@
+// kmc_device.h — device-side data layout and geometry primitives of the HIP
+// engine (gfx950).  Every arithmetic expression follows the reference's
+// operation order (main.cpp line cited at each helper) so that, compiled with
+// -ffp-contract=off, results are bit-identical to the sequential oracle.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kmc_math.h"
+#include "kmc_philox.h"
+
+namespace kmcd {
+
+// ---------------------------------------------------------------- constants
+// Derived parameters, computed once on the host with the same expressions as
+// the reference (e.g. 2*sqrt(RB_A_D*time_step/6), main.cpp:585) and passed by
+// value as a kernel argument.
+struct KParams {
+  int NA, NB, N;
+  int ncx, ncy;         // collision cell grid (xy), cs = 130 Å
+  double gx0, gy0, cs;  // grid origin and cell size
+  double box_x, box_y, box_z, pai;
+  double ra, rb;
+  double amp_a, amp_b, amp_cis, amp_bond;  // 2*sqrt(D*dt/6)
+  double rot_a, rot_b, rot_cis, rot_bond;  // sqrt(rotD*dt)
+  double p_ass, p_mono, p_cis, p_diss, p_mdiss, p_cdiss;  // rate*dt
+  double bond_cut, cis_cut, thetapd_cut, thetaot_cut, cis_theta_cut;
+  // exact squared-distance thresholds: sqrt(s) < c  <=>  s < T(c)
+  double T_aa, T_ab, T_bb, T_bond, T_cis;
+  kmcr::Key key;
+};
+
+// per-step control block in device memory (replayable without host writes)
+struct Ctl {
+  uint32_t step;          // mc_time_step being simulated
+  uint32_t obs_idx;       // record index within the current kmc_step call
+  uint32_t err;           // error bits (ERR_*)
+  uint32_t pad0;
+  // per-step work-list counters
+  uint32_t n_units;       // units (keys) this step
+  uint32_t n_overflow;    // ligands whose BFS overflowed the register queue
+  uint32_t cx_cursor;     // members[] allocation cursor
+  uint32_t n_wl[2];       // resolution work lists
+  uint32_t n_rl;          // R–L accepting edges
+  uint32_t n_cisc;        // cis candidates
+  uint32_t pad1;
+  // observables (reduced per step)
+  int32_t rl, mono, cis;  // derived from state
+  int32_t tot_prot, tot_clu, max_size;
+  int32_t off_bond, off_rl, off_cis, off_mono;  // counters − derived at load
+  int32_t maxc;                                 // protein_num_in_Max_Complex
+  int32_t pad2;
+  uint64_t vtag;          // BFS tag counter for the overflow path
+};
+
+enum : uint32_t {
+  ERR_EDGES = 1u,       // reaction edge buffer full
+  ERR_GEOMETRY = 2u,    // rigid-body extent bound violated
+  ERR_RESOLVE = 4u,     // collision resolution did not converge
+  ERR_ALIGN = 8u,       // alignment repeat guard
+  ERR_MEMBERS = 16u,    // members[] overflow
+  ERR_RECORDS = 32u,    // record buffer overflow
+};
+
+enum : uint8_t { U_NONE = 0, U_FREE_A = 1, U_DIMER = 2, U_FREE_B = 3, U_COMPLEX = 4 };
+enum : uint32_t { S_UND = 0, S_ACC = 1, S_REJ = 2 };
+
+// ---------------------------------------------------------------- layout
+// Receptor bead (j,k) (1-based) coordinate c lives at
+//   a[((((j-1)*4 + (k-1))*3 + c) * NA + i];   ligand at b[(((j-1)*2+(k-1))*3+c)*NB + i]
+// i.e. structure-of-arrays per bead coordinate: a wave's 64 lanes (64
+// consecutive proteins) load 512 contiguous bytes per bead coordinate.
+struct Beads {
+  double* a;
+  double* b;
+  int NA, NB;
+  __device__ __forceinline__ double& A(int i, int j, int k, int c) const {
+    return a[(size_t)((((j - 1) * 4 + (k - 1)) * 3) + c) * NA + i];
+  }
+  __device__ __forceinline__ double& B(int i, int j, int k, int c) const {
+    return b[(size_t)((((j - 1) * 2 + (k - 1)) * 3) + c) * NB + i];
+  }
+  // protein p is 0-based over [0, NA+NB)
+  __device__ __forceinline__ double& P(int p, int j, int k, int c) const {
+    return p < NA ? A(p, j, k, c) : B(p - NA, j, k, c);
+  }
+};
+
+// ---------------------------------------------------------------- geometry
+// Euler matrix, main.cpp:613-623
+struct Rot {
+  double t[3][3];
+};
+__device__ __forceinline__ Rot euler(double theta, double phi, double psai) {
+  double cth = kmcm::cos(theta), sth = kmcm::sin(theta);
+  double cph = kmcm::cos(phi), sph = kmcm::sin(phi);
+  double cps = kmcm::cos(psai), sps = kmcm::sin(psai);
+  Rot r;
+  r.t[0][0] = cps * cph - cth * sph * sps;
+  r.t[0][1] = -sps * cph - cth * sph * cps;
+  r.t[0][2] = sth * sph;
+  r.t[1][0] = cps * sph + cth * cph * sps;
+  r.t[1][1] = -sps * sph + cth * cph * cps;
+  r.t[1][2] = -sth * cph;
+  r.t[2][0] = sps * sth;
+  r.t[2][1] = cps * sth;
+  r.t[2][2] = cth;
+  return r;
+}
+// x' = t·(o − c) + c, one component at a time, main.cpp:631-633
+__device__ __forceinline__ double rx(const Rot& r, double ox, double oy, double oz, double cx, double cy,
+                                     double cz) {
+  return r.t[0][0] * (ox - cx) + r.t[0][1] * (oy - cy) + r.t[0][2] * (oz - cz) + cx;
+}
+__device__ __forceinline__ double ry(const Rot& r, double ox, double oy, double oz, double cx, double cy,
+                                     double cz) {
+  return r.t[1][0] * (ox - cx) + r.t[1][1] * (oy - cy) + r.t[1][2] * (oz - cz) + cy;
+}
+__device__ __forceinline__ double rz(const Rot& r, double ox, double oy, double oz, double cx, double cy,
+                                     double cz) {
+  return r.t[2][0] * (ox - cx) + r.t[2][1] * (oy - cy) + r.t[2][2] * (oz - cz) + cz;
+}
+
+// gettheta, main.cpp:2329-2366 (p1 is the origin in every call site)
+__device__ __forceinline__ double gettheta(double p0x, double p0y, double p0z, double p2x, double p2y,
+                                           double p2z) {
+  double lx0 = 0.0 - p0x, ly0 = 0.0 - p0y, lz0 = 0.0 - p0z;
+  double lr0 = kmcm::sqrt_(lx0 * lx0 + ly0 * ly0 + lz0 * lz0);
+  double lx1 = p2x - 0.0, ly1 = p2y - 0.0, lz1 = p2z - 0.0;
+  double lr1 = kmcm::sqrt_(lx1 * lx1 + ly1 * ly1 + lz1 * lz1);
+  double conv = 180 / 3.14159;
+  double doth1 = -(lx1 * lx0 + ly0 * ly1 + lz0 * lz1);
+  double doth2 = doth1 / (lr1 * lr0);
+  if (doth2 > 1) doth2 = 1;
+  if (doth2 < -1) doth2 = -1;
+  return kmcm::acos(doth2) * conv;
+}
+
+__device__ __forceinline__ bool AreSame(double a, double b) { return kmcm::fabs_(a - b) < 1.0E-8; }
+
+__device__ __forceinline__ double d2(double dx, double dy, double dz) { return dx * dx + dy * dy + dz * dz; }
+
+// relaxed agent-scope accesses for values other workgroups update in-launch
+__device__ __forceinline__ uint32_t ld_state(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_state(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+}  // namespace kmcd

@@ -1,0 +1,448 @@
+// kmc_engine.hip — C-ABI of libkmc (include/kmc.h): device memory, the
+// per-step launch sequence, state transfer.  One handle per GPU.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/kmc.h"
+#include "kmc_host.h"
+#include "kmc_kernels.hip"
+
+using namespace kmcd;
+
+struct kmc_sim {
+  kmc_params p;
+  KParams K;
+  Dev d;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int64_t step_done = 0;
+  std::string err;
+  int ncell = 0, nscan_blocks = 0;
+  bool have_state = false;
+  std::vector<void*> allocs;
+  kmc_obs_dev* obs_buf = nullptr;
+  int64_t obs_cap = 0;
+  Ctl* ctl_host = nullptr;
+  // timing
+  bool timing = false;
+  double phase_ms[8] = {0};
+  hipEvent_t ev[9] = {};
+};
+
+namespace {
+
+int fail(kmc_sim* s, int code, const std::string& m) {
+  if (s) s->err = m;
+  return code;
+}
+
+#define HIPCHK(s, x)                                                                      \
+  do {                                                                                    \
+    hipError_t e_ = (x);                                                                  \
+    if (e_ != hipSuccess)                                                                 \
+      return fail(s, KMC_ERR_HIP, std::string(#x ": ") + hipGetErrorString(e_));          \
+  } while (0)
+
+template <typename T>
+int dalloc(kmc_sim* s, T** p, size_t n) {
+  void* v = nullptr;
+  size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+  hipError_t e = hipMalloc(&v, bytes);
+  if (e != hipSuccess) return fail(s, KMC_ERR_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
+  e = hipMemset(v, 0, bytes);
+  if (e != hipSuccess) return fail(s, KMC_ERR_HIP, std::string("hipMemset: ") + hipGetErrorString(e));
+  s->allocs.push_back(v);
+  *p = (T*)v;
+  return KMC_OK;
+}
+
+// smallest T with sqrt(T) >= c, so that  sqrt(s) < c  <=>  s < T  (exact)
+double sqrt_threshold(double c) {
+  double t = c * c;
+  while (std::sqrt(t) >= c) t = std::nextafter(t, 0.0);
+  while (std::sqrt(t) < c) t = std::nextafter(t, INFINITY);
+  return t;
+}
+
+uint32_t pow2(uint32_t n) {
+  uint32_t p = 1;
+  while (p < n) p <<= 1;
+  return p;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* kmc_last_error(const kmc_sim* s) { return s ? s->err.c_str() : "null handle"; }
+
+int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
+  if (!p || !out) return KMC_ERR_ARG;
+  *out = nullptr;
+  if (p->n_a < 0 || p->n_b < 0 || p->n_a + p->n_b <= 0 || (int64_t)p->n_a + p->n_b > (1 << 24))
+    return KMC_ERR_ARG;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return KMC_ERR_NODEVICE;
+  kmc_sim* s = new kmc_sim();
+  s->p = *p;
+  if (device >= 0) {
+    if (hipSetDevice(device) != hipSuccess) {
+      delete s;
+      return KMC_ERR_NODEVICE;
+    }
+    s->device = device;
+  } else {
+    (void)hipGetDevice(&s->device);
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, s->device) != hipSuccess || std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    delete s;
+    return KMC_ERR_NODEVICE;
+  }
+  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete s;
+    return KMC_ERR_HIP;
+  }
+  KParams& K = s->K;
+  const int NA = p->n_a, NB = p->n_b, N = NA + NB;
+  K.NA = NA;
+  K.NB = NB;
+  K.N = N;
+  K.cs = 130.0;
+  K.gx0 = -p->box_x / 2 - 1000.0;
+  K.gy0 = -p->box_y / 2 - 1000.0;
+  K.ncx = std::max(1, (int)((p->box_x + 2000.0) / K.cs) + 1);
+  K.ncy = std::max(1, (int)((p->box_y + 2000.0) / K.cs) + 1);
+  K.box_x = p->box_x;
+  K.box_y = p->box_y;
+  K.box_z = p->box_z;
+  K.pai = p->pai;
+  K.ra = p->ra_radius;
+  K.rb = p->rb_radius;
+  const double ts = p->time_step;
+  // expressions as in main.cpp:585, 611, 693, 726, 909, 942, 990, 1089
+  K.amp_a = 2 * std::sqrt(p->ra_D * ts / 6);
+  K.amp_b = 2 * std::sqrt(p->rb_D * ts / 6);
+  K.amp_cis = 2 * std::sqrt(p->cis_D * ts / 6);
+  K.amp_bond = 2 * std::sqrt(p->bond_D * ts / 6);
+  K.rot_a = std::sqrt(p->ra_rot_D * ts);
+  K.rot_b = std::sqrt(p->rb_rot_D * ts);
+  K.rot_cis = std::sqrt(p->cis_rot_D * ts);
+  K.rot_bond = std::sqrt(p->bond_rot_D * ts);
+  K.p_ass = p->ass_rate * ts;
+  K.p_mono = p->mono_cis_ass_rate * ts;
+  K.p_cis = p->cis_ass_rate * ts;
+  K.p_diss = p->diss_rate * ts;
+  K.p_mdiss = p->mono_cis_diss_rate * ts;
+  K.p_cdiss = p->cis_diss_rate * ts;
+  K.bond_cut = p->bond_dist_cutoff;
+  K.cis_cut = p->cis_dist_cutoff;
+  K.thetapd_cut = p->bond_thetapd_cutoff;
+  K.thetaot_cut = p->bond_thetaot_cutoff;
+  K.cis_theta_cut = p->cis_thetaot_cutoff;
+  K.T_aa = sqrt_threshold(p->ra_radius + p->ra_radius);
+  K.T_ab = sqrt_threshold(p->ra_radius + p->rb_radius);
+  K.T_bb = sqrt_threshold(p->rb_radius + p->rb_radius);
+  K.T_bond = sqrt_threshold(p->bond_dist_cutoff);
+  K.T_cis = sqrt_threshold(p->cis_dist_cutoff);
+  K.key = kmcr::make_key(p->seed, p->replica);
+
+  s->ncell = K.ncx * K.ncy;
+  s->nscan_blocks = (s->ncell + SCAN_T * SCAN_PER - 1) / (SCAN_T * SCAN_PER);
+  Dev& d = s->d;
+  d.cur.NA = d.nxt.NA = NA;
+  d.cur.NB = d.nxt.NB = NB;
+  uint32_t cap = pow2(std::max<uint32_t>(4096, std::min<uint32_t>(1u << 20, (uint32_t)N / 8 + 1)));
+  d.cap_edges = cap;
+  int rc = KMC_OK;
+  rc |= dalloc(s, &d.cur.a, (size_t)48 * NA);
+  rc |= dalloc(s, &d.nxt.a, (size_t)48 * NA);
+  rc |= dalloc(s, &d.cur.b, (size_t)24 * NB);
+  rc |= dalloc(s, &d.nxt.b, (size_t)24 * NB);
+  rc |= dalloc(s, &d.a_int, (size_t)5 * NA);
+  rc |= dalloc(s, &d.b_int, (size_t)8 * NB);
+  rc |= dalloc(s, &d.owner, N);
+  rc |= dalloc(s, &d.ukind, N);
+  rc |= dalloc(s, &d.ustate, N);
+  rc |= dalloc(s, &d.moved, N);
+  rc |= dalloc(s, &d.cx_off, NB);
+  rc |= dalloc(s, &d.cx_size, NB);
+  rc |= dalloc(s, &d.cx_nb, NB);
+  rc |= dalloc(s, &d.members, N);
+  rc |= dalloc(s, &d.units, N);
+  rc |= dalloc(s, &d.overflow, NB);
+  rc |= dalloc(s, &d.wl0, N);
+  rc |= dalloc(s, &d.wl1, N);
+  rc |= dalloc(s, &d.cell_cnt, s->ncell);
+  rc |= dalloc(s, &d.cell_start, s->ncell + 1);
+  rc |= dalloc(s, &d.block_sums, s->nscan_blocks);
+  rc |= dalloc(s, &d.rec_pos, (size_t)2 * N);
+  rc |= dalloc(s, &d.rec_id, (size_t)2 * N);
+  rc |= dalloc(s, &d.rl_keys, cap);
+  rc |= dalloc(s, &d.cis_keys, cap);
+  rc |= dalloc(s, &d.ent, (size_t)2 * cap);
+  rc |= dalloc(s, &d.gi32, (size_t)6 * cap);
+  rc |= dalloc(s, &d.bfs_queue, N);
+  rc |= dalloc(s, &d.vtag, N);
+  rc |= dalloc(s, &d.ctl, 1);
+  if (rc != KMC_OK) {
+    kmc_destroy(s);
+    return KMC_ERR_HIP;
+  }
+  if (hipHostMalloc((void**)&s->ctl_host, sizeof(Ctl)) != hipSuccess) {
+    kmc_destroy(s);
+    return KMC_ERR_HIP;
+  }
+  for (auto& e : s->ev) (void)hipEventCreate(&e);
+  const char* tm = getenv("KMC_TIMING");
+  s->timing = tm && *tm == '1';
+  *out = s;
+  return KMC_OK;
+}
+
+int kmc_destroy(kmc_sim* s) {
+  if (!s) return KMC_OK;
+  if (s->stream) (void)hipStreamSynchronize(s->stream);
+  for (void* v : s->allocs) (void)hipFree(v);
+  if (s->obs_buf) (void)hipFree(s->obs_buf);
+  if (s->ctl_host) (void)hipHostFree(s->ctl_host);
+  for (auto& e : s->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (s->stream) (void)hipStreamDestroy(s->stream);
+  delete s;
+  return KMC_OK;
+}
+
+int64_t kmc_current_step(const kmc_sim* s) { return s ? s->step_done : -1; }
+
+int kmc_set_state(kmc_sim* s, const kmc_state_view* v) {
+  if (!s || !v) return KMC_ERR_ARG;
+  int rc = kmch_host::validate(&s->p, v, &s->err);
+  if (rc != KMC_OK) return rc;
+  const int NA = s->p.n_a, NB = s->p.n_b;
+  Dev& d = s->d;
+  HIPCHK(s, hipMemcpy(d.cur.a, v->ra, sizeof(double) * 48 * (size_t)NA, hipMemcpyHostToDevice));
+  HIPCHK(s, hipMemcpy(d.cur.b, v->rb, sizeof(double) * 24 * (size_t)NB, hipMemcpyHostToDevice));
+  HIPCHK(s, hipMemcpy(d.a_int, v->a_int, sizeof(int32_t) * 5 * (size_t)NA, hipMemcpyHostToDevice));
+  HIPCHK(s, hipMemcpy(d.b_int, v->b_int, sizeof(int32_t) * 8 * (size_t)NB, hipMemcpyHostToDevice));
+  int rl, mono, cis;
+  kmch_host::derived_counts(&s->p, v, &rl, &mono, &cis);
+  Ctl c;
+  std::memset(&c, 0, sizeof c);
+  c.step = (uint32_t)(v->step + 1);
+  // counters keep the reference's incremental bookkeeping (main.cpp:1931-2136):
+  // loaded value + change of the derived count
+  c.off_bond = v->counters[0] - (rl + mono + cis);
+  c.off_rl = v->counters[1] - rl;
+  c.off_cis = v->counters[2] - cis;
+  c.off_mono = v->counters[3] - mono;
+  c.maxc = v->counters[4];
+  HIPCHK(s, hipMemcpy(d.ctl, &c, sizeof c, hipMemcpyHostToDevice));
+  HIPCHK(s, hipMemset(d.ustate, 0, sizeof(uint32_t) * (size_t)(NA + NB)));
+  HIPCHK(s, hipMemset(d.moved, 0, sizeof(uint32_t) * (size_t)(NA + NB)));
+  s->step_done = v->step;
+  s->have_state = true;
+  return KMC_OK;
+}
+
+int kmc_get_state(kmc_sim* s, kmc_state_view* v) {
+  if (!s || !v) return KMC_ERR_ARG;
+  if (!s->have_state) return fail(s, KMC_ERR_ARG, "no state");
+  const int NA = s->p.n_a, NB = s->p.n_b;
+  Dev& d = s->d;
+  HIPCHK(s, hipStreamSynchronize(s->stream));
+  HIPCHK(s, hipMemcpy(v->ra, d.cur.a, sizeof(double) * 48 * (size_t)NA, hipMemcpyDeviceToHost));
+  HIPCHK(s, hipMemcpy(v->rb, d.cur.b, sizeof(double) * 24 * (size_t)NB, hipMemcpyDeviceToHost));
+  HIPCHK(s, hipMemcpy(v->a_int, d.a_int, sizeof(int32_t) * 5 * (size_t)NA, hipMemcpyDeviceToHost));
+  HIPCHK(s, hipMemcpy(v->b_int, d.b_int, sizeof(int32_t) * 8 * (size_t)NB, hipMemcpyDeviceToHost));
+  Ctl c;
+  HIPCHK(s, hipMemcpy(&c, d.ctl, sizeof c, hipMemcpyDeviceToHost));
+  int rl, mono, cis;
+  kmch_host::derived_counts(&s->p, v, &rl, &mono, &cis);
+  v->counters[0] = (rl + mono + cis) + c.off_bond;
+  v->counters[1] = rl + c.off_rl;
+  v->counters[2] = cis + c.off_cis;
+  v->counters[3] = mono + c.off_mono;
+  v->counters[4] = c.maxc;
+  v->step = s->step_done;
+  return KMC_OK;
+}
+
+int kmc_init_random(kmc_sim* s) {
+  if (!s) return KMC_ERR_ARG;
+  const int NA = s->p.n_a, NB = s->p.n_b;
+  std::vector<double> ra((size_t)48 * NA + 1), rb((size_t)24 * NB + 1);
+  std::vector<int32_t> ai((size_t)5 * NA + 1), bi((size_t)8 * NB + 1);
+  kmc_state_view v{ra.data(), rb.data(), ai.data(), bi.data(), {0, 0, 0, 0, 0}, 0, 0};
+  int rc = kmch_host::init_random(&s->p, &v, &s->err);
+  if (rc != KMC_OK) return rc;
+  return kmc_set_state(s, &v);
+}
+
+int kmc_load_cpt(kmc_sim* s, const char* path) {
+  if (!s || !path) return KMC_ERR_ARG;
+  const int NA = s->p.n_a, NB = s->p.n_b;
+  std::vector<double> ra((size_t)48 * NA + 1), rb((size_t)24 * NB + 1);
+  std::vector<int32_t> ai((size_t)5 * NA + 1), bi((size_t)8 * NB + 1);
+  kmc_state_view v{ra.data(), rb.data(), ai.data(), bi.data(), {0, 0, 0, 0, 0}, 0, 0};
+  int rc = kmch_host::load_cpt(&s->p, path, &v, &s->err);
+  if (rc != KMC_OK) return rc;
+  return kmc_set_state(s, &v);
+}
+
+int kmc_write_cpt(kmc_sim* s, const char* path) {
+  if (!s || !path) return KMC_ERR_ARG;
+  const int NA = s->p.n_a, NB = s->p.n_b;
+  std::vector<double> ra((size_t)48 * NA + 1), rb((size_t)24 * NB + 1);
+  std::vector<int32_t> ai((size_t)5 * NA + 1), bi((size_t)8 * NB + 1);
+  kmc_state_view v{ra.data(), rb.data(), ai.data(), bi.data(), {0, 0, 0, 0, 0}, 0, 0};
+  int rc = kmc_get_state(s, &v);
+  if (rc != KMC_OK) return rc;
+  return kmch_host::write_cpt(&s->p, &v, path, &s->err);
+}
+
+static int launch_step(kmc_sim* s) {
+  const KParams& K = s->K;
+  Dev& d = s->d;
+  hipStream_t st = s->stream;
+  const int T = 256;
+  const int gN = (K.N + T - 1) / T, gA = (K.NA + T - 1) / T, gB = (K.NB + T - 1) / T;
+  auto mark = [&](int i) {
+    if (s->timing) (void)hipEventRecord(s->ev[i], st);
+  };
+  mark(0);
+  k_begin<<<1, 1, 0, st>>>(d);
+  k_classify<<<gN, T, 0, st>>>(K, d);
+  if (K.NB > 0) {
+    k_bfs<<<gB, T, 0, st>>>(K, d);
+    k_bfs_overflow<<<1, 64, 0, st>>>(K, d);
+  }
+  mark(1);
+  k_propose<<<gN, T, 0, st>>>(K, d);
+  if (K.NB > 0) k_complex<<<gB, 64, 0, st>>>(K, d);
+  mark(2);
+  k_rec_count<<<gN, T, 0, st>>>(K, d);
+  k_scan1<<<s->nscan_blocks, SCAN_T, 0, st>>>(d.cell_cnt, d.cell_start, d.block_sums, s->ncell);
+  k_scan2<<<1, SCAN_T, 0, st>>>(d.block_sums, s->nscan_blocks, d.cell_start + s->ncell);
+  k_scan3<<<s->nscan_blocks, SCAN_T, 0, st>>>(d.cell_start, d.block_sums, s->ncell);
+  k_rec_scatter<<<gN, T, 0, st>>>(K, d);
+  mark(3);
+  k_resolve<<<gN, T, 0, st>>>(K, d, -1);
+  k_resolve<<<gN, T, 0, st>>>(K, d, 0);
+  k_resolve_tail<<<1, 1024, 0, st>>>(K, d);
+  k_commit<<<gN, T, 0, st>>>(K, d);
+  mark(4);
+  if (K.NA > 0) {
+    k_rxn_candidates<<<gA, T, 0, st>>>(K, d);
+    k_rl_match<<<1, 1024, 0, st>>>(K, d);
+    k_cis_match<<<1, 1024, 0, st>>>(K, d);
+    k_diss_rl<<<gA, T, 0, st>>>(K, d);
+    k_diss_cis<<<gA, T, 0, st>>>(K, d);
+  }
+  mark(5);
+  k_observe<<<gN, T, 0, st>>>(K, d);
+  k_finalize<<<1, 1, 0, st>>>(K, d, s->p.time_step);
+  mark(6);
+  // R_new becomes R (main.cpp:2164-2191): swap the bead buffers
+  std::swap(d.cur, d.nxt);
+  return KMC_OK;
+}
+
+int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out) {
+  if (!s) return KMC_ERR_ARG;
+  if (!s->have_state) return fail(s, KMC_ERR_ARG, "no state: call kmc_init_random / kmc_load_cpt / kmc_set_state");
+  if (nsteps <= 0) return KMC_OK;
+  static_assert(sizeof(kmc_obs_dev) == sizeof(kmc_obs), "obs layout");
+  const int64_t chunk = 4096;
+  if (!s->obs_buf) {
+    HIPCHK(s, hipMalloc((void**)&s->obs_buf, sizeof(kmc_obs_dev) * chunk));
+    s->obs_cap = chunk;
+    s->d.obs = s->obs_buf;
+  }
+  for (int i = 0; i < 8; ++i) s->phase_ms[i] = 0;
+  int64_t done = 0;
+  while (done < nsteps) {
+    int64_t n = std::min(chunk, nsteps - done);
+    uint32_t zero = 0;
+    HIPCHK(s, hipMemcpyAsync(&s->d.ctl->obs_idx, &zero, sizeof zero, hipMemcpyHostToDevice, s->stream));
+    for (int64_t k = 0; k < n; ++k) {
+      launch_step(s);
+      if (s->timing) {
+        (void)hipEventSynchronize(s->ev[6]);
+        for (int i = 0; i < 6; ++i) {
+          float ms = 0;
+          (void)hipEventElapsedTime(&ms, s->ev[i], s->ev[i + 1]);
+          s->phase_ms[i] += ms;
+        }
+      }
+    }
+    HIPCHK(s, hipGetLastError());
+    HIPCHK(s, hipMemcpyAsync(s->ctl_host, s->d.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, s->stream));
+    if (out)
+      HIPCHK(s, hipMemcpyAsync(out + done, s->obs_buf, sizeof(kmc_obs_dev) * n, hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(s, hipStreamSynchronize(s->stream));
+    s->step_done += n;
+    uint32_t err = s->ctl_host->err;
+    if (err) {
+      char m[160];
+      snprintf(m, sizeof m, "device error bits 0x%x near step %lld", err, (long long)s->step_done);
+      int code = (err & ERR_GEOMETRY) ? KMC_ERR_GEOMETRY : KMC_ERR_CAPACITY;
+      return fail(s, code, m);
+    }
+    done += n;
+  }
+  return KMC_OK;
+}
+
+// ---------------------------------------------------------------- diagnostics
+// op: 0 sin, 1 cos, 2 atan2(x, y), 3 acos, 4 sqrt, 5 x / y, 6 round
+__global__ void k_math(int op, const double* x, const double* y, double* out, int n) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double a = x[i], b = y[i], r = 0;
+  switch (op) {
+    case 0: r = kmcm::sin(a); break;
+    case 1: r = kmcm::cos(a); break;
+    case 2: r = kmcm::atan2(a, b); break;
+    case 3: r = kmcm::acos(a); break;
+    case 4: r = kmcm::sqrt_(a); break;
+    case 5: r = a / b; break;
+    default: r = kmcm::round_(a); break;
+  }
+  out[i] = r;
+}
+
+int kmc_device_math(int op, const double* x, const double* y, double* out, int64_t n) {
+  if (n <= 0) return KMC_OK;
+  double *dx = nullptr, *dy = nullptr, *dout = nullptr;
+  size_t b = sizeof(double) * (size_t)n;
+  if (hipMalloc(&dx, b) != hipSuccess || hipMalloc(&dy, b) != hipSuccess || hipMalloc(&dout, b) != hipSuccess)
+    return KMC_ERR_HIP;
+  int rc = KMC_OK;
+  if (hipMemcpy(dx, x, b, hipMemcpyHostToDevice) != hipSuccess || hipMemcpy(dy, y, b, hipMemcpyHostToDevice) != hipSuccess)
+    rc = KMC_ERR_HIP;
+  if (rc == KMC_OK) {
+    k_math<<<(int)((n + 255) / 256), 256>>>(op, dx, dy, dout, (int)n);
+    if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(out, dout, b, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = KMC_ERR_HIP;
+  }
+  (void)hipFree(dx);
+  (void)hipFree(dy);
+  (void)hipFree(dout);
+  return rc;
+}
+
+int kmc_phase_times(const kmc_sim* s, double* ms_out, int32_t n) {
+  if (!s || !ms_out) return KMC_ERR_ARG;
+  for (int i = 0; i < n && i < 8; ++i) ms_out[i] = s->phase_ms[i];
+  return 6;
+}
+
+}  // extern "C"

@@ -1,0 +1,1517 @@
+// kmc_kernels.hip — HIP/CDNA4 kernels of one KMC time step
+// (reference: /root/reference/main.cpp:461-2308).
+//
+// Parallel restatement of a sequential, order-dependent loop.  The reference
+// visits units (free receptor, cis dimer, free ligand, ligand-rooted complex)
+// in index order and tests each trial move against R_new, which already holds
+// every earlier unit's accepted move (Gauss–Seidel, main.cpp:640-664).  Here:
+//
+//   1. classify + BFS      every protein learns the key (trigger index) of the
+//                          unit that moves it; complexes get their BFS member
+//                          order (main.cpp:514-562)
+//   2. propose             every unit computes its trial move from R with its
+//                          own keyed Philox draws (independent of order)
+//   3. records             old and proposed positions of every protein go into
+//                          a 130 Å xy cell list (counting sort)
+//   4. resolve             a unit's fate depends only on lower-keyed units near
+//                          it: decided units are read, undecided ones block;
+//                          rounds until every unit is decided — exactly the
+//                          sequential outcome
+//   5. commit              rejected units copy R back into R_new
+//   6. reactions           candidate pairs from the cell list; the reference's
+//                          greedy loop order (main.cpp:1877-2058) is reproduced
+//                          as a lexicographic-first greedy matching
+//   7. dissociation, observables
+//
+// Every floating-point expression mirrors the reference's operation order;
+// the file is compiled with -ffp-contract=off.
+#include "kmc_device.h"
+
+namespace kmcd {
+
+struct Dev {
+  Beads cur, nxt;
+  int32_t* a_int;  // [5][NA]  st2 st3 nei2 nei4 nei3 (nei: reference 1-based)
+  int32_t* b_int;  // [8][NB]  st1..4 nei1..4
+  int32_t* owner;  // [N] key of the unit that moves protein p (0-based)
+  uint8_t* ukind;  // [N] unit kind keyed at p
+  uint32_t* ustate;  // [N] (step<<2)|S
+  uint32_t* moved;   // [N] step tag (main.cpp:122)
+  int32_t* cx_off;   // [NB]
+  int32_t* cx_size;  // [NB]
+  int32_t* cx_nb;    // [NB] ligands in complex
+  int32_t* members;  // [N]
+  int32_t* units;    // [N]
+  int32_t* overflow; // [NB]
+  int32_t* wl0;      // [N]
+  int32_t* wl1;      // [N]
+  int32_t* cell_cnt;    // [ncell]
+  int32_t* cell_start;  // [ncell+1]
+  int32_t* block_sums;  // [scan blocks]
+  float4* rec_pos;      // [2N]
+  int32_t* rec_id;      // [2N]  pid | isnew<<31
+  uint64_t* rl_keys;    // [cap]
+  uint64_t* cis_keys;   // [cap]
+  uint64_t* ent;        // [2*cap] greedy scratch
+  int32_t* gi32;        // [6*cap] greedy scratch
+  uint32_t cap_edges;   // power of two
+  int32_t* bfs_queue;   // [N]
+  uint32_t* vtag;       // [N]
+  Ctl* ctl;
+  struct kmc_obs_dev* obs;
+};
+
+struct kmc_obs_dev {  // == kmc_obs
+  int64_t step;
+  double t;
+  int32_t rl, mono, cis, bond;
+  double cluster_size;
+  int32_t maxc, tot_prot, tot_clu, reserved;
+};
+
+// ---------------------------------------------------------------- state access
+#define A_ST2(d, i) (d).a_int[0 * (size_t)NA + (i)]
+#define A_ST3(d, i) (d).a_int[1 * (size_t)NA + (i)]
+#define A_NEI2(d, i) (d).a_int[2 * (size_t)NA + (i)]
+#define A_NEI4(d, i) (d).a_int[3 * (size_t)NA + (i)]
+#define A_NEI3(d, i) (d).a_int[4 * (size_t)NA + (i)]
+#define B_ST(d, b, j) (d).b_int[(size_t)((j)-1) * NB + (b)]
+#define B_NEI(d, b, j) (d).b_int[(size_t)(4 + (j)-1) * NB + (b)]
+
+__device__ __forceinline__ uint32_t state_of(const Dev& d, int key, uint32_t step) {
+  if (key < 0) {  // a protein no unit claimed: inconsistent bond graph
+    atomicOr(&d.ctl->err, ERR_RESOLVE);
+    return S_REJ;
+  }
+  uint32_t v = ld_state(&d.ustate[key]);
+  return (v >> 2) == (step & 0x3fffffffu) ? (v & 3u) : S_UND;
+}
+__device__ __forceinline__ void set_state(const Dev& d, int key, uint32_t step, uint32_t s) {
+  st_state(&d.ustate[key], ((step & 0x3fffffffu) << 2) | s);
+}
+
+__device__ __forceinline__ int cell_x(const KParams& P, double x) {
+  int c = (int)__builtin_floor((x - P.gx0) / P.cs);
+  return c < 0 ? 0 : (c >= P.ncx ? P.ncx - 1 : c);
+}
+__device__ __forceinline__ int cell_y(const KParams& P, double y) {
+  int c = (int)__builtin_floor((y - P.gy0) / P.cs);
+  return c < 0 ? 0 : (c >= P.ncy ? P.ncy - 1 : c);
+}
+
+// ================================================================ step begin
+__global__ void k_begin(Dev d) {
+  Ctl* c = d.ctl;
+  c->n_units = 0;
+  c->n_overflow = 0;
+  c->cx_cursor = 0;
+  c->n_wl[0] = 0;
+  c->n_wl[1] = 0;
+  c->n_rl = 0;
+  c->n_cisc = 0;
+  c->rl = c->mono = c->cis = 0;
+  c->tot_prot = c->tot_clu = c->max_size = 0;
+}
+
+// ================================================================ 1. classify
+// Unit kinds, main.cpp:584 (free receptor), 682-686 (cis dimer, moved at the
+// lower index), 905 (single ligand = BFS component of size 1).
+__global__ void k_classify(KParams P, Dev d) {
+  const int NA = P.NA, NB = P.NB;
+  int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P.N) return;
+  uint8_t kind = U_NONE;
+  int own = -1;
+  if (p < NA) {
+    int i = p;
+    int n2 = A_NEI2(d, i), n3 = A_NEI3(d, i);
+    if (A_ST2(d, i) == 0 && A_ST3(d, i) == 0) {
+      kind = U_FREE_A;
+      own = p;
+    } else if (n2 == 0 && n3 != 0 && A_NEI3(d, n3 - 1) == i + 1 && A_NEI2(d, n3 - 1) == 0) {
+      int q = n3 - 1;
+      own = i < q ? i : q;
+      kind = i < q ? U_DIMER : U_NONE;
+    }
+  } else {
+    int b = p - NA;
+    if (B_NEI(d, b, 2) == 0 && B_NEI(d, b, 3) == 0 && B_NEI(d, b, 4) == 0) {
+      kind = U_FREE_B;
+      own = p;
+    }
+  }
+  d.ukind[p] = kind;
+  d.owner[p] = own;  // -1: complex member, set by the BFS kernels
+  if (kind != U_NONE) {
+    uint32_t s = atomicAdd(&d.ctl->n_units, 1u);
+    d.units[s] = p;
+  }
+}
+
+// ================================================================ BFS
+// Complex of ligand root b: BFS over the bond graph exactly as
+// main.cpp:525-561 (receptor neighbours res_nei[2], [3]; ligand neighbours
+// res_nei[2], [3], [4]; a node is enqueued when first seen).  The root is the
+// lowest-indexed ligand of its component; a BFS that meets a lower ligand
+// stops (that ligand owns the component).
+#define BFS_QCAP 96
+__device__ __forceinline__ int nbrs(const KParams& P, const Dev& d, int x, int* y) {
+  const int NA = P.NA, NB = P.NB;
+  int n = 0;
+  if (x < NA) {
+    int v = A_NEI2(d, x);
+    if (v > 0) y[n++] = v - 1;
+    v = A_NEI3(d, x);
+    if (v > 0) y[n++] = v - 1;
+  } else {
+    int b = x - NA;
+    for (int j = 2; j <= 4; ++j) {
+      int v = B_NEI(d, b, j);
+      if (v > 0) y[n++] = v - 1;
+    }
+  }
+  return n;
+}
+
+__device__ void register_complex(const KParams& P, const Dev& d, int p, const int* q, int qn, bool global_q) {
+  uint32_t off = atomicAdd(&d.ctl->cx_cursor, (uint32_t)qn);
+  if (off + qn > (uint32_t)P.N) {
+    atomicOr(&d.ctl->err, ERR_MEMBERS);
+    return;
+  }
+  int nb = 0;
+  for (int t = 0; t < qn; ++t) {
+    int m = q[t];
+    d.members[off + t] = m;
+    d.owner[m] = p;
+    nb += m >= P.NA;
+  }
+  int b = p - P.NA;
+  d.cx_off[b] = (int)off;
+  d.cx_size[b] = qn;
+  d.cx_nb[b] = nb;
+  d.ukind[p] = U_COMPLEX;
+  uint32_t s = atomicAdd(&d.ctl->n_units, 1u);
+  d.units[s] = p;
+  (void)global_q;
+}
+
+__global__ void k_bfs(KParams P, Dev d) {
+  const int NA = P.NA, NB = P.NB;
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= NB) return;
+  if (B_NEI(d, b, 2) == 0 && B_NEI(d, b, 3) == 0 && B_NEI(d, b, 4) == 0) return;
+  int p = NA + b;
+  int q[BFS_QCAP];
+  int qn = 0, head = 0;
+  q[qn++] = p;
+  while (head < qn) {
+    int x = q[head++];
+    int y[3];
+    int ny = nbrs(P, d, x, y);
+    for (int e = 0; e < ny; ++e) {
+      int v = y[e];
+      if (v >= NA && v < p) return;  // a lower ligand roots this component
+      bool seen = false;
+      for (int t = 0; t < qn; ++t) seen |= q[t] == v;
+      if (seen) continue;
+      if (qn == BFS_QCAP) {
+        uint32_t s = atomicAdd(&d.ctl->n_overflow, 1u);
+        d.overflow[s] = b;
+        return;
+      }
+      q[qn++] = v;
+    }
+  }
+  register_complex(P, d, p, q, qn, false);
+}
+
+// Components larger than BFS_QCAP: one thread, global queue + visit tags.
+__global__ void k_bfs_overflow(KParams P, Dev d) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const int NA = P.NA;
+  uint32_t n = d.ctl->n_overflow;
+  for (uint32_t o = 0; o < n; ++o) {
+    int p = NA + d.overflow[o];
+    uint32_t tag = (uint32_t)(++d.ctl->vtag);
+    int* q = d.bfs_queue;
+    int qn = 0, head = 0;
+    q[qn++] = p;
+    d.vtag[p] = tag;
+    bool root = true;
+    while (head < qn && root) {
+      int x = q[head++];
+      int y[3];
+      int ny = nbrs(P, d, x, y);
+      for (int e = 0; e < ny; ++e) {
+        int v = y[e];
+        if (v >= NA && v < p) {
+          root = false;
+          break;
+        }
+        if (d.vtag[v] == tag) continue;
+        d.vtag[v] = tag;
+        q[qn++] = v;
+      }
+    }
+    if (root) register_complex(P, d, p, q, qn, true);
+  }
+}
+
+// ================================================================ 2. proposals
+// free receptor, main.cpp:584-635
+__device__ void propose_free_a(const KParams& P, const Dev& d, int i, uint32_t step) {
+  double u0, u1, u2, u3;
+  kmcr::uniform2(P.key, kmcr::DOM_DIFF, (uint32_t)i, 0, step, 0, &u0, &u1);
+  kmcr::uniform2(P.key, kmcr::DOM_DIFF, (uint32_t)i, 0, step, 1, &u2, &u3);
+  double amp = P.amp_a * u0;
+  double phai = u1 * 2 * P.pai;
+  double dx = amp * kmcm::cos(phai), dy = amp * kmcm::sin(phai);
+  double o11x = d.cur.A(i, 1, 1, 0) + dx, o11y = d.cur.A(i, 1, 1, 1) + dy;
+  double PBx = P.box_x * kmcm::round_(o11x / P.box_x);
+  double PBy = P.box_y * kmcm::round_(o11y / P.box_y);
+  Rot t = euler(0, 0, (2 * u2 - 1) * P.rot_a);
+#pragma unroll
+  for (int j = 1; j <= 4; ++j) {
+    double cx = (d.cur.A(i, j, 1, 0) + dx) - PBx;
+    double cy = (d.cur.A(i, j, 1, 1) + dy) - PBy;
+    double cz = d.cur.A(i, j, 1, 2);
+    d.nxt.A(i, j, 1, 0) = cx;
+    d.nxt.A(i, j, 1, 1) = cy;
+    d.nxt.A(i, j, 1, 2) = cz;
+#pragma unroll
+    for (int k = 2; k <= 4; ++k) {
+      double ox = (d.cur.A(i, j, k, 0) + dx) - PBx;
+      double oy = (d.cur.A(i, j, k, 1) + dy) - PBy;
+      double oz = d.cur.A(i, j, k, 2);
+      d.nxt.A(i, j, k, 0) = rx(t, ox, oy, oz, cx, cy, cz);
+      d.nxt.A(i, j, k, 1) = ry(t, ox, oy, oz, cx, cy, cz);
+      d.nxt.A(i, j, k, 2) = rz(t, ox, oy, oz, cx, cy, cz);
+    }
+  }
+}
+
+// snap receptor a2 onto a1's cis site (x,y of all 16 beads), main.cpp:786-798
+__device__ void snap_cis(const KParams& P, const Beads& N, int a2, int a1, double cis_cut) {
+  const double RA = P.ra;
+  double x33 = N.A(a1, 3, 3, 0), x31 = N.A(a1, 3, 1, 0);
+  double y33 = N.A(a1, 3, 3, 1), y31 = N.A(a1, 3, 1, 1);
+  double x1 = (cis_cut / 2 + RA) / RA * (x33 - x31) + x33;
+  double y1 = (cis_cut / 2 + RA) / RA * (y33 - y31) + y33;
+  double x3 = (cis_cut / 2) / RA * (x33 - x31) + x33;
+  double y3 = (cis_cut / 2) / RA * (y33 - y31) + y33;
+  double x2 = (cis_cut / 2 + 2 * RA) / RA * (x33 - x31) + x33;
+  double y2 = (cis_cut / 2 + 2 * RA) / RA * (y33 - y31) + y33;
+  for (int k = 1; k <= 4; ++k) {
+    N.A(a2, k, 1, 0) = x1;
+    N.A(a2, k, 1, 1) = y1;
+    N.A(a2, k, 4, 0) = x1;
+    N.A(a2, k, 4, 1) = y1;
+    N.A(a2, k, 3, 0) = x3;
+    N.A(a2, k, 3, 1) = y3;
+    N.A(a2, k, 2, 0) = x2;
+    N.A(a2, k, 2, 1) = y2;
+  }
+}
+
+// snap receptor a onto ligand site (lb = ligand 0-based in B arrays, j),
+// main.cpp:1216-1228
+__device__ void snap_bond(const KParams& P, const Beads& N, int a, int lb, int j, double bond_cut) {
+  const double RA = P.ra, RB = P.rb;
+  double x2 = N.B(lb, j, 2, 0), x1 = N.B(lb, j, 1, 0);
+  double y2 = N.B(lb, j, 2, 1), y1 = N.B(lb, j, 1, 1);
+  double ax1 = (bond_cut / 2 + RA) / RB * (x2 - x1) + x2;
+  double ay1 = (bond_cut / 2 + RA) / RB * (y2 - y1) + y2;
+  double ax3 = (bond_cut / 2 + 2 * RA) / RB * (x2 - x1) + x2;
+  double ay3 = (bond_cut / 2 + 2 * RA) / RB * (y2 - y1) + y2;
+  double ax2 = (bond_cut / 2) / RB * (x2 - x1) + x2;
+  double ay2 = (bond_cut / 2) / RB * (y2 - y1) + y2;
+  for (int k = 1; k <= 4; ++k) {
+    N.A(a, k, 1, 0) = ax1;
+    N.A(a, k, 1, 1) = ay1;
+    N.A(a, k, 4, 0) = ax1;
+    N.A(a, k, 4, 1) = ay1;
+    N.A(a, k, 3, 0) = ax3;
+    N.A(a, k, 3, 1) = ay3;
+    N.A(a, k, 2, 0) = ax2;
+    N.A(a, k, 2, 1) = ay2;
+  }
+}
+
+__device__ __forceinline__ double dxyA(const Beads& N, int p, int j, int k, int q, int jj, int kk) {
+  double dx = N.A(p, j, k, 0) - N.A(q, jj, kk, 0), dy = N.A(p, j, k, 1) - N.A(q, jj, kk, 1);
+  return kmcm::sqrt_(dx * dx + dy * dy);
+}
+// ligand lb bead (j,k) vs receptor a bead (jj,kk)
+__device__ __forceinline__ double dxyBA(const Beads& N, int lb, int j, int k, int a, int jj, int kk) {
+  double dx = N.B(lb, j, k, 0) - N.A(a, jj, kk, 0), dy = N.B(lb, j, k, 1) - N.A(a, jj, kk, 1);
+  return kmcm::sqrt_(dx * dx + dy * dy);
+}
+__device__ __forceinline__ bool cis_misaligned(const KParams& P, const Beads& N, int a1, int a2) {
+  double dd2 = dxyA(N, a1, 3, 3, a2, 3, 3);
+  double dd1 = dxyA(N, a1, 3, 1, a2, 3, 1);
+  return !AreSame(dd1, P.cis_cut / 2 + P.ra + P.ra) || !AreSame(dd2, P.cis_cut / 2);
+}
+__device__ __forceinline__ bool bond_mis_d(const KParams& P, double dd1, double dd2) {
+  return !AreSame(dd1, P.bond_cut / 2 + P.ra + P.rb) || !AreSame(dd2, P.bond_cut / 2);
+}
+__device__ __forceinline__ bool bond_misaligned(const KParams& P, const Beads& N, int lb, int j, int a1) {
+  double dd2 = dxyBA(N, lb, j, 2, a1, 3, 2);
+  double dd1 = dxyBA(N, lb, j, 1, a1, 3, 1);
+  return bond_mis_d(P, dd1, dd2);
+}
+
+// cis dimer lead i with partner q, main.cpp:682-865 (proposal part)
+__device__ void propose_dimer(const KParams& P, const Dev& d, int i, int q, uint32_t step) {
+  double u0, u1, u2, u3;
+  kmcr::uniform2(P.key, kmcr::DOM_DIFF, (uint32_t)i, 0, step, 0, &u0, &u1);
+  kmcr::uniform2(P.key, kmcr::DOM_DIFF, (uint32_t)i, 0, step, 1, &u2, &u3);
+  double amp = P.amp_cis * u0;
+  double phai = u1 * 2 * P.pai;
+  double dx = amp * kmcm::cos(phai), dy = amp * kmcm::sin(phai);
+  double PBx = P.box_x * kmcm::round_(((d.cur.A(i, 1, 1, 0) + dx) + (d.cur.A(q, 1, 1, 0) + dx)) / 2 / P.box_x);
+  double PBy = P.box_y * kmcm::round_(((d.cur.A(i, 1, 1, 1) + dy) + (d.cur.A(q, 1, 1, 1) + dy)) / 2 / P.box_y);
+  Rot t = euler(0, 0, (2 * u2 - 1) * P.rot_cis);
+  // rotation centre: R_new before the move (= R), main.cpp:740-753
+  double cmx = 0, cmy = 0, cmz = 0;
+  for (int j = 1; j <= 4; ++j) {
+    cmx = cmx + d.cur.A(i, j, 1, 0) + d.cur.A(q, j, 1, 0);
+    cmy = cmy + d.cur.A(i, j, 1, 1) + d.cur.A(q, j, 1, 1);
+    cmz = cmz + d.cur.A(i, j, 1, 2) + d.cur.A(q, j, 1, 2);
+  }
+  cmx = cmx / (4 * 2);
+  cmy = cmy / (4 * 2);
+  cmz = cmz / (4 * 2);
+  for (int w = 0; w < 2; ++w) {
+    int a = w ? q : i;
+    for (int j = 1; j <= 4; ++j)
+      for (int k = 1; k <= 4; ++k) {
+        double ox = (d.cur.A(a, j, k, 0) + dx) - PBx;
+        double oy = (d.cur.A(a, j, k, 1) + dy) - PBy;
+        double oz = d.cur.A(a, j, k, 2);
+        d.nxt.A(a, j, k, 0) = rx(t, ox, oy, oz, cmx, cmy, cmz);
+        d.nxt.A(a, j, k, 1) = ry(t, ox, oy, oz, cmx, cmy, cmz);
+        d.nxt.A(a, j, k, 2) = rz(t, ox, oy, oz, cmx, cmy, cmz);
+      }
+  }
+  // relax, main.cpp:770-799
+  double dist2 = dxyA(d.nxt, i, 3, 3, q, 3, 3);
+  double dist1 = dxyA(d.nxt, i, 3, 1, q, 3, 1);
+  double dist3 = P.cis_cut / 2 + P.ra + P.ra;
+  double dist4 = P.cis_cut / 2;
+  if (!AreSame(dist1, dist3) || !AreSame(dist2, dist4)) snap_cis(P, d.nxt, q, i, P.cis_cut);
+}
+
+// single ligand, main.cpp:905-969
+__device__ void propose_free_b(const KParams& P, const Dev& d, int lb, int p, uint32_t step) {
+  double u[6];
+  kmcr::uniform2(P.key, kmcr::DOM_DIFF, (uint32_t)p, 0, step, 0, &u[0], &u[1]);
+  kmcr::uniform2(P.key, kmcr::DOM_DIFF, (uint32_t)p, 0, step, 1, &u[2], &u[3]);
+  kmcr::uniform2(P.key, kmcr::DOM_DIFF, (uint32_t)p, 0, step, 2, &u[4], &u[5]);
+  double amp = P.amp_b * u[0];
+  double theta = u[1] * P.pai;
+  double phai = u[2] * 2 * P.pai;
+  double sth = kmcm::sin(theta), cth = kmcm::cos(theta);
+  double dx = amp * sth * kmcm::cos(phai);
+  double dy = amp * sth * kmcm::sin(phai);
+  double dz = amp * cth;
+  double o11x = d.cur.B(lb, 1, 1, 0) + dx, o11y = d.cur.B(lb, 1, 1, 1) + dy, o11z = d.cur.B(lb, 1, 1, 2) + dz;
+  double PBx = P.box_x * kmcm::round_(o11x / P.box_x);
+  double PBy = P.box_y * kmcm::round_(o11y / P.box_y);
+  double PBz = P.box_z * kmcm::round_(o11z / P.box_z);
+  bool refl = o11z > P.box_z || o11z < 0;
+  Rot t = euler((2 * u[3] - 1) * P.rot_b, (2 * u[4] - 1) * P.rot_b, (2 * u[5] - 1) * P.rot_b);
+  double ox[4][2], oy[4][2], oz[4][2];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      double z = d.cur.B(lb, j + 1, k + 1, 2) + dz;
+      if (refl) z = -z + 2 * PBz;
+      oz[j][k] = z;
+      ox[j][k] = (d.cur.B(lb, j + 1, k + 1, 0) + dx) - PBx;
+      oy[j][k] = (d.cur.B(lb, j + 1, k + 1, 1) + dy) - PBy;
+    }
+  // R_new[1][1] = R_new0[1][1], then every bead (incl. [1][1] itself, which
+  // updates the centre in place) rotates about R_new[1][1], main.cpp:958-968
+  double cx = ox[0][0], cy = oy[0][0], cz = oz[0][0];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      double nx = rx(t, ox[j][k], oy[j][k], oz[j][k], cx, cy, cz);
+      if (j == 0 && k == 0) cx = nx;
+      double ny = ry(t, ox[j][k], oy[j][k], oz[j][k], cx, cy, cz);
+      if (j == 0 && k == 0) cy = ny;
+      double nz = rz(t, ox[j][k], oy[j][k], oz[j][k], cx, cy, cz);
+      if (j == 0 && k == 0) cz = nz;
+      d.nxt.B(lb, j + 1, k + 1, 0) = nx;
+      d.nxt.B(lb, j + 1, k + 1, 1) = ny;
+      d.nxt.B(lb, j + 1, k + 1, 2) = nz;
+    }
+}
+
+__global__ void k_propose(KParams P, Dev d) {
+  int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P.N) return;
+  const uint32_t step = d.ctl->step;
+  const int NA = P.NA;
+  uint8_t k = d.ukind[p];
+  if (k == U_FREE_A) propose_free_a(P, d, p, step);
+  else if (k == U_DIMER) propose_dimer(P, d, p, A_NEI3(d, p) - 1, step);
+  else if (k == U_FREE_B) propose_free_b(P, d, p - P.NA, p, step);
+}
+
+// ---------------------------------------------------------------- complexes
+// Ligand-rooted complex of size > 1: rigid move (main.cpp:974-1131), lay-down
+// of a single ligand (1138-1193), receptor / cis re-alignment (1196-1274),
+// multi-ligand alignment (1284-1732).  One thread per complex runs the
+// sequential code on R (d.cur) and R_new (d.nxt).
+struct Cx {
+  const KParams& P;
+  const Dev& d;
+  uint32_t step;
+  int root;  // protein index of the root ligand
+  int* res;  // member row (BFS order, shuffled in place like results[c][.])
+  int size;
+  __device__ bool isA(int m) const { return m < P.NA; }
+  __device__ double& N(int m, int j, int k, int c) const { return d.nxt.P(m, j, k, c); }
+  __device__ double& R(int m, int j, int k, int c) const { return d.cur.P(m, j, k, c); }
+  __device__ int nk(int m) const { return m < P.NA ? 4 : 2; }
+  __device__ int neiA2(int a) const { const int NA = P.NA; return A_NEI2(d, a); }
+  __device__ int neiA3(int a) const { const int NA = P.NA; return A_NEI3(d, a); }
+  __device__ int neiA4(int a) const { const int NA = P.NA; return A_NEI4(d, a); }
+  __device__ int neiB(int lb, int j) const { const int NB = P.NB; return B_NEI(d, lb, j); }
+  // res_nei_new[x][j] with reference semantics for the alignment code, where
+  // x may be a receptor or a ligand (reference index, 0 = the empty row 0)
+  __device__ int rnei(int x_ref, int j) const {
+    if (x_ref <= 0) return 0;
+    int x = x_ref - 1;
+    if (x < P.NA) return j == 2 ? neiA2(x) : j == 3 ? neiA3(x) : j == 4 ? neiA4(x) : 0;
+    return j >= 1 && j <= 4 ? neiB(x - P.NA, j) : 0;
+  }
+  __device__ bool is_moved(int m) const { return d.moved[m] == step + 1; }
+  __device__ void set_moved(int m) const { d.moved[m] = step + 1; }
+  __device__ uint32_t shuf_rand(uint32_t call, uint32_t pos) const {
+    return kmcr::rand31(P.key, kmcr::DOM_SHUF, (uint32_t)root, call, step, pos);
+  }
+  // libstdc++ random_shuffle over res[0 .. size-2] (main.cpp:1285)
+  __device__ void shuffle(uint32_t call) const {
+    for (int i = 1; i < size - 1; ++i) {
+      int j = (int)(shuf_rand(call, (uint32_t)i) % (uint32_t)(i + 1));
+      if (i != j) {
+        int tmp = res[i];
+        res[i] = res[j];
+        res[j] = tmp;
+      }
+    }
+  }
+};
+
+__device__ void ligand_template(double rb, double tx[5][3], double ty[5][3]) {
+  for (int j = 0; j < 5; ++j)
+    for (int k = 0; k < 3; ++k) tx[j][k] = ty[j][k] = 0;
+  const double s3 = kmcm::sqrt_(3.0);
+  tx[2][1] = 0; ty[2][1] = rb * 2 / s3;
+  tx[2][2] = 0; ty[2][2] = rb * (2 / s3 + 1);
+  tx[3][1] = -rb; ty[3][1] = -rb / s3;
+  tx[3][2] = -rb * (s3 / 2 + 1); ty[3][2] = -rb / s3 - rb / 2;
+  tx[4][1] = rb; ty[4][1] = -rb / s3;
+  tx[4][2] = rb * (s3 / 2 + 1); ty[4][2] = -rb / s3 - rb / 2;
+}
+
+// body of lable4, main.cpp:1441-1583; returns protein_B_index (0-based) after it
+__device__ int step2_body(const Cx& X, int B, int j, int a1) {
+  const KParams& P = X.P;
+  const Beads& N = X.d.nxt;
+  const int NA = P.NA;
+  X.set_moved(B);
+  int lb = B - NA;
+  double za = N.A(a1, 3, 1, 2);
+  for (int k = 1; k <= 2; ++k) {
+    N.B(lb, 1, k, 2) = za;
+    N.B(lb, 2, k, 2) = za;
+    N.B(lb, 3, k, 2) = za;
+    N.B(lb, 4, k, 2) = za;
+  }
+  N.B(lb, 1, 2, 2) = N.A(a1, 3, 1, 2) + P.rb;
+  double tx[5][3], ty[5][3];
+  ligand_template(P.rb, tx, ty);
+  double ax1 = tx[j][1], ay1 = ty[j][1];
+  double ax2 = N.A(a1, 3, 1, 0) - N.A(a1, 3, 2, 0);
+  double ay2 = N.A(a1, 3, 1, 1) - N.A(a1, 3, 2, 1);
+  double dot = ax1 * ax2 + ay1 * ay2;
+  double det = ax1 * ay2 - ay1 * ax2;
+  double angle = kmcm::atan2(-det, -dot) + P.pai;
+  const double s3 = kmcm::sqrt_(3.0);
+  double cmx = (P.bond_cut / 2 + P.rb * 2 / s3 + P.rb) / P.ra * (N.A(a1, 3, 2, 0) - N.A(a1, 3, 1, 0)) + N.A(a1, 3, 2, 0);
+  double cmy = (P.bond_cut / 2 + P.rb * 2 / s3 + P.rb) / P.ra * (N.A(a1, 3, 2, 1) - N.A(a1, 3, 1, 1)) + N.A(a1, 3, 2, 1);
+  double ca = kmcm::cos(angle), sa = kmcm::sin(angle);
+  for (int m = 1; m <= 4; ++m)
+    for (int n = 1; n <= 2; ++n) {
+      N.B(lb, m, n, 0) = tx[m][n] * ca - ty[m][n] * sa + cmx;
+      N.B(lb, m, n, 1) = tx[m][n] * sa + ty[m][n] * ca + cmy;
+    }
+  int Bref = B + 1;  // protein_B_index in reference numbering
+  for (int m = 2; m <= 4; ++m) {
+    int A1ref = X.rnei(Bref, m);
+    if (X.rnei(A1ref, 2) != 0) {
+      Bref = X.rnei(A1ref, 2);
+      int n = X.rnei(A1ref, 4);
+      int A1 = A1ref - 1, lb2 = Bref - 1 - NA;
+      if (bond_misaligned(P, N, lb2, n, A1)) {
+        X.set_moved(A1);
+        snap_bond(P, N, A1, lb2, n, P.bond_cut);
+      }
+      if (X.rnei(A1ref, 3) != 0) {
+        int A2 = X.rnei(A1ref, 3) - 1;
+        if (cis_misaligned(P, N, A1, A2)) {
+          X.set_moved(A2);
+          snap_cis(P, N, A2, A1, P.cis_cut);
+        }
+      }
+    }
+  }
+  return Bref - 1;
+}
+
+__device__ void multi_ligand_align(const Cx& X) {
+  const KParams& P = X.P;
+  const Beads& N = X.d.nxt;
+  const int NA = P.NA;
+  const int csize = X.size;
+  int* res = X.res;
+  uint32_t call = 0;
+  // step 0, main.cpp:1284-1332
+  X.shuffle(call++);
+  for (int csi = 0; csi < csize; ++csi) {
+    int m = res[csi];
+    if (m < NA && X.neiA2(m) != 0) {
+      int lb = X.neiA2(m) - 1 - NA, j = X.neiA4(m);
+      if (bond_misaligned(P, N, lb, j, m)) {
+        X.set_moved(m);
+        snap_bond(P, N, m, lb, j, P.bond_cut);
+      }
+    }
+  }
+  // step 1, main.cpp:1341-1406
+  X.shuffle(call++);
+  for (int csi = 0; csi < csize; ++csi) {
+    int pa = res[csi];
+    if (pa < NA) {
+      if (X.neiA2(pa) != 0 && X.neiA3(pa) != 0 && X.rnei(X.neiA3(pa), 2) != 0 && !X.is_moved(pa)) {
+        int a1 = pa, a2 = X.neiA3(a1) - 1;
+        X.set_moved(a1);
+        X.set_moved(a2);
+        double dd1 = dxyA(N, a1, 3, 1, a2, 3, 1);
+        double dd2 = dxyA(N, a1, 3, 3, a2, 3, 3);
+        if (!AreSame(dd1, P.cis_cut / 2 + P.ra + P.ra) || !AreSame(dd2, P.cis_cut / 2)) snap_cis(P, N, a1, a2, P.cis_cut);
+      }
+    }
+  }
+  // step 2 (main.cpp:1411-1590) + repeat (1595-1635): the goto lable4 re-enters
+  // the step-2 loop body at the repeat scan's (member, site) position
+  X.shuffle(call++);
+  int start_csi = 0, start_j = 2;
+  bool jump = false;
+  int jB = 0, jA1 = 0;
+  double jd1 = 0, jd2 = 0;
+  for (int guard = 0;; ++guard) {
+    if (guard > 4 * csize + 8) {
+      atomicOr(&X.d.ctl->err, ERR_ALIGN);
+      return;
+    }
+    for (int csi = start_csi; csi < csize; ++csi) {
+      int B = res[csi];
+      if (jump) B = jB;
+      if (B >= NA) {
+        for (int j = jump ? start_j : 2; j <= 4; ++j) {
+          int a1;
+          double dist1, dist2;
+          if (jump) {
+            jump = false;
+            a1 = jA1;
+            dist1 = jd1;
+            dist2 = jd2;
+          } else {
+            int Bref = B + 1;
+            int A1ref = X.rnei(Bref, j);
+            if (!(A1ref != 0 && X.rnei(A1ref, 3) != 0 && X.rnei(X.rnei(A1ref, 3), 2) != 0 && !X.is_moved(B)))
+              continue;
+            a1 = A1ref - 1;
+            dist2 = dxyBA(N, B - NA, j, 2, a1, 3, 2);
+            dist1 = dxyBA(N, B - NA, j, 1, a1, 3, 1);
+          }
+          if (bond_mis_d(P, dist1, dist2)) B = step2_body(X, B, j, a1);
+        }
+      }
+    }
+    X.shuffle(call++);
+    bool again = false;
+    for (int csi = 0; csi < csize && !again; ++csi) {
+      int B = res[csi];
+      if (B < NA) continue;
+      for (int j = 2; j <= 4; ++j) {
+        int Bref = B + 1;
+        int A1ref = X.rnei(Bref, j);
+        if (A1ref != 0 && X.rnei(A1ref, 3) != 0 && X.rnei(X.rnei(A1ref, 3), 2) != 0 && !X.is_moved(B)) {
+          int a1 = A1ref - 1;
+          double dd2 = dxyBA(N, B - NA, j, 2, a1, 3, 2);
+          double dd1 = dxyBA(N, B - NA, j, 1, a1, 3, 1);
+          if (bond_mis_d(P, dd1, dd2)) {
+            again = true;
+            jump = true;
+            start_csi = csi;
+            start_j = j;
+            jB = B;
+            jA1 = a1;
+            jd1 = dd1;
+            jd2 = dd2;
+            break;
+          }
+        }
+      }
+    }
+    if (!again) break;
+  }
+  // step 3, main.cpp:1645-1687
+  for (int csi = 0; csi < csize; ++csi) {
+    int m = res[csi];
+    if (m < NA && X.neiA2(m) != 0) {
+      int lb = X.neiA2(m) - 1 - NA, j = X.neiA4(m);
+      if (bond_misaligned(P, N, lb, j, m)) {
+        X.set_moved(m);
+        snap_bond(P, N, m, lb, j, P.bond_cut);
+      }
+    }
+  }
+  // step 4, main.cpp:1691-1732
+  for (int csi = 0; csi < csize; ++csi) {
+    int m = res[csi];
+    if (m < NA && X.neiA2(m) != 0 && X.neiA3(m) != 0 && X.rnei(X.neiA3(m), 2) == 0) {
+      int a2 = X.neiA3(m) - 1;
+      if (cis_misaligned(P, N, m, a2)) snap_cis(P, N, a2, m, P.cis_cut);
+    }
+  }
+}
+
+__global__ void k_complex(KParams P, Dev d) {
+  int lb = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lb >= P.NB) return;
+  int p = P.NA + lb;
+  if (d.ukind[p] != U_COMPLEX) return;
+  const int NA = P.NA;
+  const uint32_t step = d.ctl->step;
+  Cx X{P, d, step, p, d.members + d.cx_off[lb], d.cx_size[lb]};
+  int* res = X.res;
+  const int csize = X.size;
+  int nB = d.cx_nb[lb], nA = csize - nB;
+  // rigid move, main.cpp:974-1131
+  double u0, u1, u2, u3;
+  kmcr::uniform2(P.key, kmcr::DOM_DIFF, (uint32_t)p, 0, step, 0, &u0, &u1);
+  kmcr::uniform2(P.key, kmcr::DOM_DIFF, (uint32_t)p, 0, step, 1, &u2, &u3);
+  double amp = (nB == 1 ? P.amp_bond : 0.0) * u0;
+  double phai = u1 * 2 * P.pai;
+  double dx = amp * kmcm::cos(phai), dy = amp * kmcm::sin(phai);
+  double PBx = 0, PBy = 0;
+  for (int t = 0; t < csize; ++t) {
+    int m = res[t];
+    PBx = PBx + (X.R(m, 1, 1, 0) + dx);
+    PBy = PBy + (X.R(m, 1, 1, 1) + dy);
+  }
+  PBx = P.box_x * kmcm::round_(PBx / (nA + nB) / P.box_x);
+  PBy = P.box_y * kmcm::round_(PBy / (nA + nB) / P.box_y);
+  double cmx = 0, cmy = 0, cmz = 0;
+  for (int t = 0; t < csize; ++t) {
+    int m = res[t];
+    for (int j = 1; j <= 4; ++j) {
+      cmx = cmx + ((X.R(m, j, 1, 0) + dx) - PBx);
+      cmy = cmy + ((X.R(m, j, 1, 1) + dy) - PBy);
+      cmz = cmz + X.R(m, j, 1, 2);
+    }
+  }
+  cmx = cmx / (4 * nA + 4 * nB);
+  cmy = cmy / (4 * nA + 4 * nB);
+  cmz = cmz / (4 * nA + 4 * nB);
+  Rot t = euler(0, 0, (2 * u2 - 1) * (nB == 1 ? P.rot_bond : 0.0));
+  int pA = -1, pB = -1;
+  for (int q = 0; q < csize; ++q) {
+    int m = res[q];
+    int nk = X.nk(m);
+    for (int j = 1; j <= 4; ++j)
+      for (int k = 1; k <= nk; ++k) {
+        double ox = (X.R(m, j, k, 0) + dx) - PBx;
+        double oy = (X.R(m, j, k, 1) + dy) - PBy;
+        double oz = X.R(m, j, k, 2);
+        X.N(m, j, k, 0) = rx(t, ox, oy, oz, cmx, cmy, cmz);
+        X.N(m, j, k, 1) = ry(t, ox, oy, oz, cmx, cmy, cmz);
+        X.N(m, j, k, 2) = rz(t, ox, oy, oz, cmx, cmy, cmz);
+      }
+    if (m < NA) pA = m;
+    else pB = m;
+  }
+  const Beads& N = d.nxt;
+  if (nB == 1) {
+    int lbB = pB - NA;
+    // lay-down, main.cpp:1140-1193 (exact != test)
+    if (N.B(lbB, 1, 2, 2) != (N.B(lbB, 1, 1, 2) + P.rb)) {
+      for (int j = 1; j <= 4; ++j)
+        for (int k = 1; k <= 2; ++k) N.B(lbB, j, k, 2) = N.A(pA, 3, 1, 2);
+      N.B(lbB, 1, 2, 2) = N.A(pA, 3, 1, 2) + P.rb;
+      double angle = kmcm::atan2((N.B(lbB, 2, 1, 0) - N.B(lbB, 1, 1, 0)), (N.B(lbB, 2, 1, 1) - N.B(lbB, 1, 1, 1))) + P.pai;
+      double tx[5][3], ty[5][3];
+      ligand_template(P.rb, tx, ty);
+      double c0x = N.B(lbB, 1, 1, 0), c0y = N.B(lbB, 1, 1, 1);
+      double ca = kmcm::cos(angle), sa = kmcm::sin(angle);
+      for (int j = 1; j <= 4; ++j)
+        for (int k = 1; k <= 2; ++k) {
+          N.B(lbB, j, k, 0) = tx[j][k] * ca - ty[j][k] * sa + c0x;
+          N.B(lbB, j, k, 1) = tx[j][k] * sa + ty[j][k] * ca + c0y;
+        }
+    }
+    // align attached receptors, main.cpp:1196-1233
+    for (int j = 2; j <= 4; ++j) {
+      int a1ref = X.neiB(lbB, j);
+      if (a1ref != 0 && bond_misaligned(P, N, lbB, j, a1ref - 1)) snap_bond(P, N, a1ref - 1, lbB, j, P.bond_cut);
+    }
+    // align their cis partners, main.cpp:1237-1274
+    for (int j = 2; j <= 4; ++j) {
+      int a1ref = X.neiB(lbB, j);
+      if (a1ref != 0 && X.neiA3(a1ref - 1) != 0) {
+        int a1 = a1ref - 1, a2 = X.neiA3(a1) - 1;
+        if (cis_misaligned(P, N, a1, a2)) snap_cis(P, N, a2, a1, P.cis_cut);
+      }
+    }
+  }
+  if (nB > 1) multi_ligand_align(X);
+}
+
+// ================================================================ 3. records
+__device__ __forceinline__ void ref_point(const Dev& d, const Beads& B, int p, int NA, double& x, double& y,
+                                          double& zlo, double& zhi) {
+  if (p < NA) {
+    x = B.A(p, 1, 1, 0);
+    y = B.A(p, 1, 1, 1);
+    zlo = B.A(p, 1, 1, 2);
+    zhi = B.A(p, 4, 1, 2);
+  } else {
+    x = B.B(p - NA, 1, 1, 0);
+    y = B.B(p - NA, 1, 1, 1);
+    zlo = B.B(p - NA, 1, 1, 2);
+    zhi = zlo;
+  }
+}
+
+// rigid-body extent bound the 3x3 stencil relies on (DESIGN.md §cell list)
+__device__ __forceinline__ bool extent_ok(const Beads& B, int p, int NA) {
+  if (p < NA) {
+    double x0 = B.A(p, 1, 1, 0), y0 = B.A(p, 1, 1, 1);
+    for (int j = 2; j <= 4; ++j) {
+      double dx = B.A(p, j, 1, 0) - x0, dy = B.A(p, j, 1, 1) - y0;
+      if (!(dx * dx + dy * dy <= 0.09)) return false;
+    }
+    return true;
+  }
+  int b = p - NA;
+  double x0 = B.B(b, 1, 1, 0), y0 = B.B(b, 1, 1, 1);
+  for (int j = 2; j <= 4; ++j) {
+    double dx = B.B(b, j, 1, 0) - x0, dy = B.B(b, j, 1, 1) - y0;
+    if (!(dx * dx + dy * dy <= 35.0 * 35.0)) return false;
+  }
+  return true;
+}
+
+__global__ void k_rec_count(KParams P, Dev d) {
+  int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P.N) return;
+  double x, y, zl, zh;
+  ref_point(d, d.cur, p, P.NA, x, y, zl, zh);
+  atomicAdd(&d.cell_cnt[cell_y(P, y) * P.ncx + cell_x(P, x)], 1);
+  ref_point(d, d.nxt, p, P.NA, x, y, zl, zh);
+  atomicAdd(&d.cell_cnt[cell_y(P, y) * P.ncx + cell_x(P, x)], 1);
+  if (!extent_ok(d.nxt, p, P.NA)) atomicOr(&d.ctl->err, ERR_GEOMETRY);
+}
+
+// exclusive scan of cell_cnt[0..n) into cell_start[0..n]; 3 kernels
+#define SCAN_T 1024
+#define SCAN_PER 4
+__global__ void k_scan1(const int32_t* in, int32_t* out, int32_t* sums, int n) {
+  __shared__ int32_t s[SCAN_T];
+  int base = (blockIdx.x * SCAN_T + threadIdx.x) * SCAN_PER;
+  int v[SCAN_PER];
+  int tot = 0;
+#pragma unroll
+  for (int q = 0; q < SCAN_PER; ++q) {
+    v[q] = base + q < n ? in[base + q] : 0;
+    tot += v[q];
+  }
+  s[threadIdx.x] = tot;
+  __syncthreads();
+  for (int off = 1; off < SCAN_T; off <<= 1) {
+    int t = threadIdx.x >= off ? s[threadIdx.x - off] : 0;
+    __syncthreads();
+    s[threadIdx.x] += t;
+    __syncthreads();
+  }
+  int run = s[threadIdx.x] - tot;
+#pragma unroll
+  for (int q = 0; q < SCAN_PER; ++q) {
+    if (base + q < n) out[base + q] = run;
+    run += v[q];
+  }
+  if (threadIdx.x == SCAN_T - 1) sums[blockIdx.x] = s[SCAN_T - 1];
+}
+__global__ void k_scan2(int32_t* sums, int nb, int32_t* total_out) {
+  __shared__ int32_t s[SCAN_T];
+  int carry = 0;
+  for (int base = 0; base < nb; base += SCAN_T) {
+    int i = base + threadIdx.x;
+    int v = i < nb ? sums[i] : 0;
+    s[threadIdx.x] = v;
+    __syncthreads();
+    for (int off = 1; off < SCAN_T; off <<= 1) {
+      int t = threadIdx.x >= off ? s[threadIdx.x - off] : 0;
+      __syncthreads();
+      s[threadIdx.x] += t;
+      __syncthreads();
+    }
+    if (i < nb) sums[i] = carry + s[threadIdx.x] - v;
+    int blk = s[SCAN_T - 1];
+    __syncthreads();
+    carry += blk;
+  }
+  if (threadIdx.x == 0) *total_out = carry;
+}
+__global__ void k_scan3(int32_t* out, const int32_t* sums, int n) {
+  int base = (blockIdx.x * SCAN_T + threadIdx.x) * SCAN_PER;
+  int add = sums[blockIdx.x];
+#pragma unroll
+  for (int q = 0; q < SCAN_PER; ++q)
+    if (base + q < n) out[base + q] += add;
+}
+
+__global__ void k_rec_scatter(KParams P, Dev d) {
+  int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P.N) return;
+  for (int w = 0; w < 2; ++w) {
+    double x, y, zl, zh;
+    ref_point(d, w ? d.nxt : d.cur, p, P.NA, x, y, zl, zh);
+    int c = cell_y(P, y) * P.ncx + cell_x(P, x);
+    int pos = d.cell_start[c] + atomicSub(&d.cell_cnt[c], 1) - 1;  // leaves cell_cnt zeroed
+    d.rec_pos[pos] = make_float4((float)x, (float)y, (float)zl, (float)zh);
+    d.rec_id[pos] = p | (w << 31);
+  }
+}
+
+// ================================================================ 4. resolve
+// Exact pair tests, main.cpp:640-664 (A vs A [1][1] < 2RA; A domains vs B
+// subunits < RA+RB), 1798-1826 (B subunits vs B subunits < 2RB; vs A domains).
+// sqrt(s) < c is evaluated as s < T(c) (T precomputed exactly on the host).
+struct Own {
+  double x[4], y[4], z[4];  // receptor domains [k][1] k=1..4 or ligand subunits [k][1] k=2..4 (idx 1..3)
+  bool isA;
+};
+__device__ __forceinline__ void load_own(const KParams& P, const Beads& B, int m, Own& o) {
+  o.isA = m < P.NA;
+  if (o.isA) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      o.x[k] = B.A(m, k + 1, 1, 0);
+      o.y[k] = B.A(m, k + 1, 1, 1);
+      o.z[k] = B.A(m, k + 1, 1, 2);
+    }
+  } else {
+    int b = m - P.NA;
+    o.x[0] = B.B(b, 1, 1, 0);
+    o.y[0] = B.B(b, 1, 1, 1);
+    o.z[0] = B.B(b, 1, 1, 2);
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      o.x[k] = B.B(b, k + 1, 1, 0);
+      o.y[k] = B.B(b, k + 1, 1, 1);
+      o.z[k] = B.B(b, k + 1, 1, 2);
+    }
+  }
+}
+
+__device__ bool exact_collide(const KParams& P, const Own& o, const Beads& B, int q) {
+  const int NA = P.NA;
+  if (o.isA) {
+    if (q < NA) {
+      double dx = B.A(q, 1, 1, 0) - o.x[0], dy = B.A(q, 1, 1, 1) - o.y[0], dz = B.A(q, 1, 1, 2) - o.z[0];
+      return d2(dx, dy, dz) < P.T_aa;
+    }
+    int b = q - NA;
+    for (int j = 2; j <= 4; ++j) {
+      double qx = B.B(b, j, 1, 0), qy = B.B(b, j, 1, 1), qz = B.B(b, j, 1, 2);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (d2(qx - o.x[k], qy - o.y[k], qz - o.z[k]) < P.T_ab) return true;
+    }
+    return false;
+  }
+  if (q >= NA) {
+    int b = q - NA;
+    for (int j = 2; j <= 4; ++j) {
+      double qx = B.B(b, j, 1, 0), qy = B.B(b, j, 1, 1), qz = B.B(b, j, 1, 2);
+#pragma unroll
+      for (int k = 1; k < 4; ++k)
+        if (d2(qx - o.x[k], qy - o.y[k], qz - o.z[k]) < P.T_bb) return true;
+    }
+    return false;
+  }
+  for (int j = 1; j <= 4; ++j) {
+    double qx = B.A(q, j, 1, 0), qy = B.A(q, j, 1, 1), qz = B.A(q, j, 1, 2);
+#pragma unroll
+    for (int k = 1; k < 4; ++k)
+      if (d2(qx - o.x[k], qy - o.y[k], qz - o.z[k]) < P.T_ab) return true;
+  }
+  return false;
+}
+
+// conservative single-precision prefilter on reference points (margins ≥ 1 Å
+// cover float rounding and the rigid-body extents)
+__device__ __forceinline__ bool prefilter(bool mA, float mx, float my, float mzl, float mzh, bool qA, float4 r) {
+  float dx = r.x - mx, dy = r.y - my;
+  float dxy2 = dx * dx + dy * dy;
+  if (mA && qA) {
+    float dz = r.z - mzl;
+    return dxy2 + dz * dz < 42.0f * 42.0f;
+  }
+  if (!mA && !qA) {
+    float dz = r.z - mzl;
+    return dxy2 + dz * dz < 131.5f * 131.5f;
+  }
+  // receptor axis [zlo, zhi] vs ligand centre
+  float lz, alo, ahi;
+  if (mA) {
+    lz = r.z;
+    alo = mzl;
+    ahi = mzh;
+  } else {
+    lz = mzl;
+    alo = r.z;
+    ahi = r.w;
+  }
+  if (!(dxy2 < 86.5f * 86.5f)) return false;
+  return lz > alo - 86.5f && lz < ahi + 86.5f;
+}
+
+__device__ uint32_t evaluate_unit(const KParams& P, const Dev& d, int u, uint32_t step) {
+  const int NA = P.NA;
+  uint8_t kind = d.ukind[u];
+  int nm;
+  const int* mem = nullptr;
+  int two[2];
+  if (kind == U_COMPLEX) {
+    int lb = u - NA;
+    nm = d.cx_size[lb];
+    mem = d.members + d.cx_off[lb];
+  } else if (kind == U_DIMER) {
+    two[0] = u;
+    two[1] = A_NEI3(d, u) - 1;
+    nm = 2;
+    mem = two;
+  } else {
+    two[0] = u;
+    nm = 1;
+    mem = two;
+  }
+  bool blocked = false;
+  for (int t = 0; t < nm; ++t) {
+    int m = mem[t];
+    Own o;
+    load_own(P, d.nxt, m, o);
+    float mx = (float)o.x[0], my = (float)o.y[0], mzl = (float)o.z[0];
+    float mzh = o.isA ? (float)o.z[3] : mzl;
+    int cx = cell_x(P, o.x[0]), cy = cell_y(P, o.y[0]);
+    for (int yy = cy - 1; yy <= cy + 1; ++yy) {
+      if (yy < 0 || yy >= P.ncy) continue;
+      int x0 = cx > 0 ? cx - 1 : 0, x1 = cx + 1 < P.ncx ? cx + 1 : P.ncx - 1;
+      int r0 = d.cell_start[yy * P.ncx + x0], r1 = d.cell_start[yy * P.ncx + x1 + 1];
+      for (int r = r0; r < r1; ++r) {
+        int id = d.rec_id[r];
+        int q = id & 0x7fffffff;
+        bool isnew = id < 0;
+        if (q == m) continue;
+        int kq = d.owner[q];
+        bool pending = false;
+        if (kq < 0) {
+          atomicOr(&d.ctl->err, ERR_RESOLVE);
+          continue;
+        }
+        if (kq == u) {
+          if (!isnew) continue;
+        } else if (kq > u) {
+          if (isnew) continue;
+        } else {
+          uint32_t s = state_of(d, kq, step);
+          if (s == S_ACC) {
+            if (!isnew) continue;
+          } else if (s == S_REJ) {
+            if (isnew) continue;
+          } else {
+            pending = true;
+          }
+        }
+        if (!prefilter(o.isA, mx, my, mzl, mzh, q < NA, d.rec_pos[r])) continue;
+        if (exact_collide(P, o, isnew ? d.nxt : d.cur, q)) {
+          if (!pending) return S_REJ;
+          blocked = true;
+        }
+      }
+    }
+  }
+  return blocked ? S_UND : S_ACC;
+}
+
+__global__ void k_resolve(KParams P, Dev d, int src) {
+  const uint32_t step = d.ctl->step;
+  uint32_t n = src < 0 ? d.ctl->n_units : d.ctl->n_wl[src];
+  const int32_t* list = src < 0 ? d.units : (src == 0 ? d.wl0 : d.wl1);
+  int32_t* dst = src < 0 ? d.wl0 : d.wl1;
+  uint32_t* ndst = src < 0 ? &d.ctl->n_wl[0] : &d.ctl->n_wl[1];
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+    int u = list[t];
+    uint32_t s = evaluate_unit(P, d, u, step);
+    if (s == S_UND) {
+      uint32_t pos = atomicAdd(ndst, 1u);
+      dst[pos] = u;
+    } else {
+      set_state(d, u, step, s);
+    }
+  }
+}
+
+// single-workgroup tail: iterate until every unit is decided; the lowest
+// undecided key always decides, so this terminates
+__global__ void __launch_bounds__(1024) k_resolve_tail(KParams P, Dev d) {
+  __shared__ uint32_t n_next, n_cur;
+  __shared__ int flip;
+  const uint32_t step = d.ctl->step;
+  if (threadIdx.x == 0) {
+    n_cur = d.ctl->n_wl[1];
+    flip = 0;
+  }
+  __syncthreads();
+  uint32_t guard = 0;
+  while (n_cur > 0) {
+    if (threadIdx.x == 0) n_next = 0;
+    __syncthreads();
+    int32_t* src = flip ? d.wl0 : d.wl1;
+    int32_t* dst = flip ? d.wl1 : d.wl0;
+    for (uint32_t t = threadIdx.x; t < n_cur; t += blockDim.x) {
+      int u = src[t];
+      uint32_t s = evaluate_unit(P, d, u, step);
+      if (s == S_UND) dst[atomicAdd(&n_next, 1u)] = u;
+      else set_state(d, u, step, s);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      n_cur = n_next;
+      flip ^= 1;
+    }
+    __syncthreads();
+    if (++guard > (uint32_t)P.N + 2) {
+      if (threadIdx.x == 0) atomicOr(&d.ctl->err, ERR_RESOLVE);
+      break;
+    }
+  }
+}
+
+// ================================================================ 5. commit
+__global__ void k_commit(KParams P, Dev d) {
+  int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P.N) return;
+  const uint32_t step = d.ctl->step;
+  uint32_t s = state_of(d, d.owner[p], step);
+  if (s == S_ACC) return;
+  if (s != S_REJ) {
+    atomicOr(&d.ctl->err, ERR_RESOLVE);
+    return;
+  }
+  if (p < P.NA) {
+    for (int r = 0; r < 48; ++r) d.nxt.a[(size_t)r * P.NA + p] = d.cur.a[(size_t)r * P.NA + p];
+  } else {
+    int b = p - P.NA;
+    for (int r = 0; r < 24; ++r) d.nxt.b[(size_t)r * P.NB + b] = d.cur.b[(size_t)r * P.NB + b];
+  }
+}
+
+// ================================================================ 6. reactions
+__device__ __forceinline__ bool record_final(const Dev& d, int id, uint32_t step) {
+  int q = id & 0x7fffffff;
+  bool isnew = id < 0;
+  uint32_t s = state_of(d, d.owner[q], step);
+  return isnew ? s == S_ACC : s == S_REJ;
+}
+
+// Candidate pairs (after diffusion, from R_new): R–L association gates
+// main.cpp:1880-1921 and cis gates 1954-1985 / 2009-2039.  A pair becomes an
+// accepting edge when its keyed draw is below the acceptance probability;
+// the greedy kernels below replay the reference's loop order on those edges.
+__global__ void k_rxn_candidates(KParams P, Dev d) {
+  const int NA = P.NA, NB = P.NB;
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= NA) return;
+  const uint32_t step = d.ctl->step;
+  const Beads& N = d.nxt;
+  bool want_rl = A_ST2(d, i) == 0 && NB > 0;
+  bool want_cis = A_ST3(d, i) == 0;
+  if (!want_rl && !want_cis) return;
+  double ax = N.A(i, 1, 1, 0), ay = N.A(i, 1, 1, 1);
+  float fx = (float)ax, fy = (float)ay, fzl = (float)N.A(i, 1, 1, 2), fzh = (float)N.A(i, 4, 1, 2);
+  int cx = cell_x(P, ax), cy = cell_y(P, ay);
+  for (int yy = cy - 1; yy <= cy + 1; ++yy) {
+    if (yy < 0 || yy >= P.ncy) continue;
+    int x0 = cx > 0 ? cx - 1 : 0, x1 = cx + 1 < P.ncx ? cx + 1 : P.ncx - 1;
+    int r0 = d.cell_start[yy * P.ncx + x0], r1 = d.cell_start[yy * P.ncx + x1 + 1];
+    for (int r = r0; r < r1; ++r) {
+      int id = d.rec_id[r];
+      int q = id & 0x7fffffff;
+      if (q == i) continue;
+      float4 rp = d.rec_pos[r];
+      float dx = rp.x - fx, dy = rp.y - fy;
+      float dxy2 = dx * dx + dy * dy;
+      if (q >= NA) {
+        if (!want_rl) continue;
+        if (!(dxy2 < 105.0f * 105.0f) || !(rp.z > fzl - 85.0f && rp.z < fzh + 85.0f)) continue;
+        if (!record_final(d, id, step)) continue;
+        int lb = q - NA;
+        for (int k = 2; k <= 4; ++k) {
+          if (B_ST(d, lb, k) != 0) continue;
+          double ddx = N.B(lb, k, 2, 0) - N.A(i, 3, 2, 0), ddy = N.B(lb, k, 2, 1) - N.A(i, 3, 2, 1),
+                 ddz = N.B(lb, k, 2, 2) - N.A(i, 3, 2, 2);
+          if (!(d2(ddx, ddy, ddz) < P.T_bond)) continue;
+          double ot = gettheta(N.A(i, 3, 1, 0) - N.A(i, 3, 2, 0), N.A(i, 3, 1, 1) - N.A(i, 3, 2, 1),
+                               N.A(i, 3, 1, 2) - N.A(i, 3, 2, 2), N.B(lb, k, 1, 0) - N.B(lb, k, 2, 0),
+                               N.B(lb, k, 1, 1) - N.B(lb, k, 2, 1), N.B(lb, k, 1, 2) - N.B(lb, k, 2, 2));
+          double pd = gettheta(N.A(i, 3, 1, 0) - N.A(i, 3, 4, 0), N.A(i, 3, 1, 1) - N.A(i, 3, 4, 1),
+                               N.A(i, 3, 1, 2) - N.A(i, 3, 4, 2), N.B(lb, 1, 1, 0) - N.B(lb, 1, 2, 0),
+                               N.B(lb, 1, 1, 1) - N.B(lb, 1, 2, 1), N.B(lb, 1, 1, 2) - N.B(lb, 1, 2, 2));
+          if (!((kmcm::fabs_(pd) < P.thetapd_cut) && (kmcm::fabs_(ot - 180) < P.thetaot_cut))) continue;
+          double u = kmcr::uniform(P.key, kmcr::DOM_RL, (uint32_t)i, (uint32_t)q, step, (uint32_t)k);
+          if (!(u < P.p_ass)) continue;
+          uint32_t pos = atomicAdd(&d.ctl->n_rl, 1u);
+          if (pos < d.cap_edges)
+            d.rl_keys[pos] = ((uint64_t)i << 34) | ((uint64_t)q << 2) | (uint64_t)(k - 2);
+          else
+            atomicOr(&d.ctl->err, ERR_EDGES);
+        }
+      } else {
+        if (!want_cis || A_ST3(d, q) != 0) continue;
+        float dz = rp.z - fzl;
+        if (!(dxy2 < 57.0f * 57.0f) || !(dz * dz < 16.0f * 16.0f + 1.0f)) continue;
+        if (!record_final(d, id, step)) continue;
+        double ddx = N.A(q, 3, 3, 0) - N.A(i, 3, 3, 0), ddy = N.A(q, 3, 3, 1) - N.A(i, 3, 3, 1),
+               ddz = N.A(q, 3, 3, 2) - N.A(i, 3, 3, 2);
+        if (!(d2(ddx, ddy, ddz) < P.T_cis)) continue;
+        double ot = gettheta(N.A(i, 3, 1, 0) - N.A(i, 3, 3, 0), N.A(i, 3, 1, 1) - N.A(i, 3, 3, 1),
+                             N.A(i, 3, 1, 2) - N.A(i, 3, 3, 2), N.A(q, 3, 1, 0) - N.A(q, 3, 3, 0),
+                             N.A(q, 3, 1, 1) - N.A(q, 3, 3, 1), N.A(q, 3, 1, 2) - N.A(q, 3, 3, 2));
+        if (!(kmcm::fabs_(ot - 180) < P.cis_theta_cut)) continue;
+        double um = kmcr::uniform(P.key, kmcr::DOM_MONO, (uint32_t)i, (uint32_t)q, step, 0);
+        double uc = kmcr::uniform(P.key, kmcr::DOM_CIS, (uint32_t)i, (uint32_t)q, step, 0);
+        uint64_t fl = (um < P.p_mono ? 1u : 0u) | (uc < P.p_cis ? 2u : 0u);
+        if (!fl) continue;
+        uint32_t pos = atomicAdd(&d.ctl->n_cisc, 1u);
+        if (pos < d.cap_edges)
+          d.cis_keys[pos] = ((uint64_t)i << 34) | ((uint64_t)q << 2) | fl;
+        else
+          atomicOr(&d.ctl->err, ERR_EDGES);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- greedy
+// In-place bitonic sort of keys[0..np) (np a power of two) by one workgroup.
+__device__ void block_sort(uint64_t* keys, uint32_t np) {
+  for (uint32_t k = 2; k <= np; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) {
+        uint32_t l = i ^ j;
+        if (l > i) {
+          uint64_t a = keys[i], b = keys[l];
+          bool up = (i & k) == 0;
+          if ((a > b) == up) {
+            keys[i] = b;
+            keys[l] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t pow2ceil(uint32_t n) {
+  uint32_t p = 1;
+  while (p < n) p <<= 1;
+  return p;
+}
+
+// Lexicographic-first greedy matching: edges (sorted keys[0..n)) are taken in
+// order; an edge is accepted iff no earlier edge sharing one of its two
+// vertices was accepted — the outcome of the reference's nested loops with
+// in-place status updates.  Parallel form: per-vertex chains in edge order;
+// an edge decides once both chain predecessors have decided.
+// vtx(e, w) gives the two vertex ids of edge e.  acc[e] receives the result.
+template <typename VF>
+__device__ void block_greedy(uint32_t n, const uint64_t* keys, VF vtx, uint64_t* ent, int32_t* g, uint8_t* acc,
+                             uint32_t* err) {
+  // g layout: pos[2n] | pred[2n] | dec[n]   (ent: 2n vertex entries)
+  int32_t* pos = g;
+  int32_t* pred = g + 2 * n;
+  int32_t* dec = g + 4 * n;
+  uint8_t* chain = acc + n;  // 2n flags after acc[n]
+  uint32_t np = pow2ceil(2 * n);
+  for (uint32_t e = threadIdx.x; e < np; e += blockDim.x) {
+    if (e < 2 * n) ent[e] = ((uint64_t)vtx(keys[e >> 1], e & 1) << 32) | e;  // entry = (vertex, 2e+w)
+    else ent[e] = ~0ull;
+  }
+  __syncthreads();
+  block_sort(ent, np);
+  for (uint32_t x = threadIdx.x; x < 2 * n; x += blockDim.x) {
+    uint32_t ew = (uint32_t)ent[x];
+    pos[ew] = (int32_t)x;
+    pred[x] = (x > 0 && (ent[x - 1] >> 32) == (ent[x] >> 32)) ? (int32_t)(x - 1) : -1;
+  }
+  for (uint32_t e = threadIdx.x; e < n; e += blockDim.x) dec[e] = 0;
+  __syncthreads();
+  __shared__ int any_left;
+  for (int round = 1;; ++round) {
+    if (threadIdx.x == 0) any_left = 0;
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < n; e += blockDim.x) {
+      if (dec[e]) continue;
+      bool ready = true, blocked = false;
+      int px[2];
+      for (int w = 0; w < 2; ++w) {
+        px[w] = pred[pos[2 * e + w]];
+        if (px[w] >= 0) {
+          uint32_t pe = ((uint32_t)ent[px[w]]) >> 1;
+          int dr = dec[pe];
+          if (dr == 0 || dr == round) ready = false;
+          else blocked |= chain[px[w]] != 0;
+        }
+      }
+      if (!ready) {
+        any_left = 1;
+        continue;
+      }
+      uint8_t a = blocked ? 0 : 1;
+      acc[e] = a;
+      for (int w = 0; w < 2; ++w) chain[pos[2 * e + w]] = (uint8_t)(a | (px[w] >= 0 ? chain[px[w]] : 0));
+      dec[e] = round;
+    }
+    __syncthreads();
+    if (!any_left) break;
+    if (round > (int)n + 2) {
+      if (threadIdx.x == 0) atomicOr(err, ERR_EDGES);
+      break;
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+}
+
+struct RLV {
+  int N;
+  __device__ uint32_t operator()(uint64_t key, int w) const {
+    if (w == 0) return (uint32_t)(key >> 34);  // receptor
+    uint32_t q = (uint32_t)((key >> 2) & 0xffffffffu), k = (uint32_t)(key & 3u);
+    return (uint32_t)N + (q - (uint32_t)0) * 4u + k;  // ligand site (distinct id space)
+  }
+};
+struct CisV {
+  __device__ uint32_t operator()(uint64_t key, int w) const {
+    return w == 0 ? (uint32_t)(key >> 34) : (uint32_t)((key >> 2) & 0xffffffffu);
+  }
+};
+
+// R–L association, main.cpp:1877-1949
+__global__ void __launch_bounds__(1024) k_rl_match(KParams P, Dev d) {
+  const int NA = P.NA, NB = P.NB;
+  uint32_t n = d.ctl->n_rl;
+  if (n == 0) return;
+  if (n > d.cap_edges) n = d.cap_edges;
+  uint32_t np = pow2ceil(n);
+  for (uint32_t e = n + threadIdx.x; e < np; e += blockDim.x) d.rl_keys[e] = ~0ull;
+  __syncthreads();
+  block_sort(d.rl_keys, np);
+  uint8_t* acc = (uint8_t*)(d.gi32 + 5 * d.cap_edges);
+  block_greedy(n, d.rl_keys, RLV{P.N}, d.ent, d.gi32, acc, &d.ctl->err);
+  for (uint32_t e = threadIdx.x; e < n; e += blockDim.x) {
+    if (!acc[e]) continue;
+    uint64_t key = d.rl_keys[e];
+    int i = (int)(key >> 34), q = (int)((key >> 2) & 0xffffffffu), k = (int)(key & 3) + 2;
+    int lb = q - NA;
+    A_ST2(d, i) = 1;
+    B_ST(d, lb, k) = 1;
+    B_NEI(d, lb, k) = i + 1;
+    A_NEI2(d, i) = q + 1;
+    A_NEI4(d, i) = k;
+  }
+}
+
+// cis association: mono (main.cpp:1952-2003) then complex (2007-2058)
+__global__ void __launch_bounds__(1024) k_cis_match(KParams P, Dev d) {
+  const int NA = P.NA;
+  uint32_t n0 = d.ctl->n_cisc;
+  if (n0 == 0) return;
+  if (n0 > d.cap_edges) n0 = d.cap_edges;
+  uint64_t* keys = d.cis_keys;
+  uint8_t* acc = (uint8_t*)(d.gi32 + 5 * d.cap_edges);
+  __shared__ uint32_t m;
+  for (int pass = 0; pass < 2; ++pass) {
+    // edges of this pass go to the back half of rl_keys as scratch
+    uint64_t* e = d.rl_keys;
+    if (threadIdx.x == 0) m = 0;
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < n0; t += blockDim.x) {
+      uint64_t key = keys[t];
+      int i = (int)(key >> 34), q = (int)((key >> 2) & 0xffffffffu);
+      uint32_t fl = (uint32_t)(key & 3);
+      bool unb = A_ST2(d, i) == 0 && A_ST2(d, q) == 0;
+      bool ok = pass == 0 ? (unb && (fl & 1)) : (!unb && (fl & 2) && A_ST3(d, i) == 0 && A_ST3(d, q) == 0);
+      if (ok) e[atomicAdd(&m, 1u)] = key & ~3ull;
+    }
+    __syncthreads();
+    uint32_t n = m;
+    if (n > 0) {
+      uint32_t np = pow2ceil(n);
+      for (uint32_t t = n + threadIdx.x; t < np; t += blockDim.x) e[t] = ~0ull;
+      __syncthreads();
+      block_sort(e, np);
+      block_greedy(n, e, CisV{}, d.ent, d.gi32, acc, &d.ctl->err);
+      for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) {
+        if (!acc[t]) continue;
+        int i = (int)(e[t] >> 34), q = (int)((e[t] >> 2) & 0xffffffffu);
+        A_ST3(d, i) = 1;
+        A_ST3(d, q) = 1;
+        A_NEI3(d, q) = i + 1;
+        A_NEI3(d, i) = q + 1;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// R–L dissociation, main.cpp:2063-2092 (one bond per receptor: independent)
+__global__ void k_diss_rl(KParams P, Dev d) {
+  const int NA = P.NA, NB = P.NB;
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= NA) return;
+  if (A_ST2(d, i) != 1) return;
+  const uint32_t step = d.ctl->step;
+  double u = kmcr::uniform(P.key, kmcr::DOM_RLD, (uint32_t)i, 0, step, 0);
+  if (!(u < P.p_diss)) return;
+  int q = A_NEI2(d, i) - 1, k = A_NEI4(d, i);
+  int lb = q - NA;
+  A_ST2(d, i) = 0;
+  B_ST(d, lb, k) = 0;
+  A_NEI2(d, i) = 0;
+  A_NEI4(d, i) = 0;
+  B_NEI(d, lb, k) = 0;
+}
+
+// cis dissociation, mono (main.cpp:2097-2117) and complex (2120-2141): both
+// members of a pair draw in index order, so a pair breaks iff either draw
+// succeeds; handled by the lower index
+__global__ void k_diss_cis(KParams P, Dev d) {
+  const int NA = P.NA;
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= NA) return;
+  if (A_ST3(d, i) != 1) return;
+  int q = A_NEI3(d, i) - 1;
+  if (q < i) return;
+  const uint32_t step = d.ctl->step;
+  bool mono = A_ST2(d, i) == 0 && A_ST2(d, q) == 0;
+  uint32_t dom = mono ? kmcr::DOM_MD : kmcr::DOM_CD;
+  double pd = mono ? P.p_mdiss : P.p_cdiss;
+  double ui = kmcr::uniform(P.key, dom, (uint32_t)i, 0, step, 0);
+  double uq = kmcr::uniform(P.key, dom, (uint32_t)q, 0, step, 0);
+  if (ui < pd || uq < pd) {
+    A_ST3(d, i) = 0;
+    A_ST3(d, q) = 0;
+    A_NEI3(d, i) = 0;
+    A_NEI3(d, q) = 0;
+  }
+}
+
+// ================================================================ 7. observables
+__device__ __forceinline__ int wave_sum(int v) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  return v;
+}
+__device__ __forceinline__ int wave_max(int v) {
+  for (int off = 32; off > 0; off >>= 1) {
+    int o = __shfl_down(v, off, 64);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
+__global__ void k_observe(KParams P, Dev d) {
+  const int NA = P.NA;
+  int p = blockIdx.x * blockDim.x + threadIdx.x;
+  int rl = 0, mono = 0, cis = 0, tp = 0, tc = 0, mx = 0;
+  if (p < NA) {
+    rl = A_ST2(d, p);
+    if (A_ST3(d, p) == 1) {
+      int q = A_NEI3(d, p) - 1;
+      if (p < q) {
+        if (A_ST2(d, p) == 0 && A_ST2(d, q) == 0) mono = 1;
+        else cis = 1;
+      }
+    }
+  } else if (p < P.N) {
+    uint8_t k = d.ukind[p];
+    if (k == U_COMPLEX) {
+      int s = d.cx_size[p - NA];
+      tp = s;
+      tc = 1;
+      mx = s;
+    } else if (k == U_FREE_B) {
+      mx = 1;
+    }
+  }
+  rl = wave_sum(rl);
+  mono = wave_sum(mono);
+  cis = wave_sum(cis);
+  tp = wave_sum(tp);
+  tc = wave_sum(tc);
+  mx = wave_max(mx);
+  if ((threadIdx.x & 63) == 0) {
+    if (rl) atomicAdd(&d.ctl->rl, rl);
+    if (mono) atomicAdd(&d.ctl->mono, mono);
+    if (cis) atomicAdd(&d.ctl->cis, cis);
+    if (tp) atomicAdd(&d.ctl->tot_prot, tp);
+    if (tc) atomicAdd(&d.ctl->tot_clu, tc);
+    if (mx) atomicMax(&d.ctl->max_size, mx);
+  }
+}
+
+// bond.dat record (main.cpp:2195-2202, 2251) and step advance
+__global__ void k_finalize(KParams P, Dev d, double time_step) {
+  Ctl* c = d.ctl;
+  if (c->max_size > c->maxc) c->maxc = c->max_size;
+  kmc_obs_dev o;
+  o.step = (int64_t)c->step;
+  o.t = (double)(int)c->step * time_step;
+  o.rl = c->rl + c->off_rl;
+  o.mono = c->mono + c->off_mono;
+  o.cis = c->cis + c->off_cis;
+  o.bond = (c->rl + c->mono + c->cis) + c->off_bond;
+  o.cluster_size = c->tot_clu != 0 ? (double)c->tot_prot / c->tot_clu : 0.0;
+  o.maxc = c->maxc;
+  o.tot_prot = c->tot_prot;
+  o.tot_clu = c->tot_clu;
+  o.reserved = 0;
+  d.obs[c->obs_idx] = o;
+  c->obs_idx = c->obs_idx + 1;
+  c->step = c->step + 1;
+}
+
+}  // namespace kmcd

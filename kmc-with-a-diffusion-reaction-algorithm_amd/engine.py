@@ -1,0 +1,203 @@
+"""Python host mirror of the reference's step-loop contract over libkmc.
+
+The reference is one process that owns its state in globals and talks
+through files (main.cpp:169-278, 2206-2305).  `Simulation` is the same
+contract as an object: construct with the physics parameters (the
+reference's compile-time globals, main.cpp:39-99), obtain an initial state
+(random placement, main.cpp:281-447, or position.cpt, main.cpp:226-270),
+advance the diffusion–reaction loop (main.cpp:461-2308) on the GPU, read the
+bond.dat observables, write position.cpt.
+
+Everything runs in libkmc (HIP kernels on gfx950); this module only
+marshals host buffers.  There is no CPU fallback: if the library or a gfx950
+device is missing, construction raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional
+
+import numpy as np
+
+from . import capi
+
+_lib = None
+
+
+class KmcError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{capi.ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+def load_library(path: Optional[str] = None):
+    """Load libkmc.so (built in-tree by build.py).  Raises if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = path or capi.LIB_PATH
+    if not os.path.exists(path):
+        raise KmcError(-9, f"{path} not built (run __graft_entry__.build())")
+    L = C.CDLL(path)
+    P = C.POINTER
+    L.kmc_params_default.argtypes = [P(capi.Params)]
+    L.kmc_create.argtypes = [P(capi.Params), C.c_int, P(C.c_void_p)]
+    L.kmc_destroy.argtypes = [C.c_void_p]
+    L.kmc_last_error.restype = C.c_char_p
+    L.kmc_last_error.argtypes = [C.c_void_p]
+    L.kmc_init_random.argtypes = [C.c_void_p]
+    L.kmc_load_cpt.argtypes = [C.c_void_p, C.c_char_p]
+    L.kmc_write_cpt.argtypes = [C.c_void_p, C.c_char_p]
+    L.kmc_set_state.argtypes = [C.c_void_p, P(capi.StateView)]
+    L.kmc_get_state.argtypes = [C.c_void_p, P(capi.StateView)]
+    L.kmc_step.argtypes = [C.c_void_p, C.c_int64, C.c_void_p]
+    L.kmc_current_step.restype = C.c_int64
+    L.kmc_current_step.argtypes = [C.c_void_p]
+    L.kmc_phase_times.argtypes = [C.c_void_p, P(C.c_double), C.c_int32]
+    L.kmc_format_bond_line.argtypes = [P(capi.Params), P(capi.Obs), C.c_char_p, C.c_size_t]
+    L.kmc_state_hash.restype = C.c_uint64
+    L.kmc_state_hash.argtypes = [P(capi.Params), P(capi.StateView)]
+    L.kmc_host_last_error.restype = C.c_char_p
+    L.kmc_host_load_cpt.argtypes = [P(capi.Params), C.c_char_p, P(capi.StateView)]
+    L.kmc_host_write_cpt.argtypes = [P(capi.Params), P(capi.StateView), C.c_char_p]
+    L.kmc_host_init_random.argtypes = [P(capi.Params), P(capi.StateView)]
+    L.kmc_host_validate.argtypes = [P(capi.Params), P(capi.StateView)]
+    for f in ("kmc_host_math", "kmc_device_math"):
+        getattr(L, f).argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]
+    _lib = L
+    return L
+
+
+def _host_check(rc: int):
+    if rc != 0:
+        raise KmcError(rc, load_library().kmc_host_last_error().decode())
+
+
+# ---------------------------------------------------------------- host-only
+def host_init_random(params: capi.Params) -> capi.HostState:
+    """Random placement (main.cpp:281-447, keyed draws) into host buffers."""
+    hs = capi.HostState(params.n_a, params.n_b)
+    v = hs.view()
+    _host_check(load_library().kmc_host_init_random(C.byref(params), C.byref(v)))
+    hs.pull(v)
+    return hs
+
+
+def host_load_cpt(params: capi.Params, path: str) -> capi.HostState:
+    """position.cpt → host state (main.cpp:226-270)."""
+    hs = capi.HostState(params.n_a, params.n_b)
+    v = hs.view()
+    _host_check(load_library().kmc_host_load_cpt(C.byref(params), os.fsencode(path), C.byref(v)))
+    hs.pull(v)
+    return hs
+
+
+def host_write_cpt(params: capi.Params, hs: capi.HostState, path: str) -> None:
+    """host state → position.cpt (main.cpp:2206-2244)."""
+    v = hs.view()
+    _host_check(load_library().kmc_host_write_cpt(C.byref(params), C.byref(v), os.fsencode(path)))
+
+
+def host_validate(params: capi.Params, hs: capi.HostState) -> int:
+    v = hs.view()
+    return int(load_library().kmc_host_validate(C.byref(params), C.byref(v)))
+
+
+def state_hash(params: capi.Params, hs: capi.HostState) -> int:
+    v = hs.view()
+    return int(load_library().kmc_state_hash(C.byref(params), C.byref(v)))
+
+
+def bond_line(params: capi.Params, rec) -> str:
+    """One bond.dat line (main.cpp:2251) from a kmc_obs record."""
+    o = capi.Obs()
+    for name in capi.OBS_DTYPE.names:
+        setattr(o, name, rec[name].item() if hasattr(rec[name], "item") else rec[name])
+    buf = C.create_string_buffer(256)
+    n = load_library().kmc_format_bond_line(C.byref(params), C.byref(o), buf, 256)
+    return buf.value[:n].decode()
+
+
+def math(op: int, x: np.ndarray, y: Optional[np.ndarray] = None, device: bool = False) -> np.ndarray:
+    """Portable libm (kmc_math.h) on host or device — numerics diagnostics."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.ascontiguousarray(np.zeros_like(x) if y is None else y, dtype=np.float64)
+    out = np.empty_like(x)
+    L = load_library()
+    f = L.kmc_device_math if device else L.kmc_host_math
+    rc = f(op, x.ctypes.data, y.ctypes.data, out.ctypes.data, x.size)
+    if rc != 0:
+        raise KmcError(rc, "math diagnostic failed")
+    return out
+
+
+# ---------------------------------------------------------------- device sim
+class Simulation:
+    """One trajectory on one GPU (handle = kmc_sim*)."""
+
+    def __init__(self, params: capi.Params, device: int = 0):
+        self.params = params
+        L = load_library()
+        h = C.c_void_p()
+        rc = L.kmc_create(C.byref(params), device, C.byref(h))
+        if rc != 0:
+            raise KmcError(rc, "kmc_create failed (needs a gfx950 device)")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load_library().kmc_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc: int):
+        if rc != 0:
+            raise KmcError(rc, load_library().kmc_last_error(self._h).decode())
+
+    def init_random(self):
+        self._check(load_library().kmc_init_random(self._h))
+
+    def load_cpt(self, path: str):
+        self._check(load_library().kmc_load_cpt(self._h, os.fsencode(path)))
+
+    def write_cpt(self, path: str):
+        self._check(load_library().kmc_write_cpt(self._h, os.fsencode(path)))
+
+    def set_state(self, hs: capi.HostState):
+        v = hs.view()
+        self._check(load_library().kmc_set_state(self._h, C.byref(v)))
+
+    def get_state(self) -> capi.HostState:
+        hs = capi.HostState(self.params.n_a, self.params.n_b)
+        v = hs.view()
+        self._check(load_library().kmc_get_state(self._h, C.byref(v)))
+        hs.pull(v)
+        return hs
+
+    def step(self, n: int, out: Optional[np.ndarray] = None) -> np.ndarray:
+        """Advance n steps; returns the n bond.dat records (capi.OBS_DTYPE)."""
+        if out is None:
+            out = np.zeros(n, dtype=capi.OBS_DTYPE)
+        self._check(load_library().kmc_step(self._h, n, out.ctypes.data_as(C.c_void_p)))
+        return out
+
+    @property
+    def current_step(self) -> int:
+        return int(load_library().kmc_current_step(self._h))
+
+    def phase_times(self) -> np.ndarray:
+        buf = (C.c_double * 8)()
+        n = load_library().kmc_phase_times(self._h, buf, 8)
+        return np.array(buf[:n])

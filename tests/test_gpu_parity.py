@@ -1,0 +1,104 @@
+"""GPU parity: the HIP engine (through the C-ABI) against the keyed CPU oracle.
+
+Bit-exact: every coordinate, status, link and counter after every step
+(FNV-1a hash of the full state) and every bond.dat observable.
+"""
+import numpy as np
+import pytest
+
+from _kmc import DENSE, O, capi, engine, params
+
+pytestmark = pytest.mark.gpu
+
+OPS = {"sin": 0, "cos": 1, "atan2": 2, "acos": 3, "sqrt": 4, "div": 5, "round": 6}
+
+
+@pytest.mark.parametrize("op", list(OPS))
+def test_device_math_bitexact(op):
+    rng = np.random.default_rng(OPS[op])
+    n = 1 << 18
+    if op == "acos":
+        x = rng.uniform(-1.0, 1.0, n)
+    elif op == "sqrt":
+        x = np.abs(rng.standard_normal(n)) * 10.0 ** rng.integers(-3, 12, n)
+    else:
+        x = rng.uniform(-20.0, 20.0, n) * 10.0 ** rng.integers(-6, 4, n)
+    y = rng.uniform(-20.0, 20.0, n)
+    x[:8] = [0.0, -0.0, 1.0, -1.0, 0.5, -0.5, 2.5, -2.5]
+    h = engine.math(OPS[op], x, y, device=False)
+    d = engine.math(OPS[op], x, y, device=True)
+    bad = np.flatnonzero(h.view(np.uint64) != d.view(np.uint64))
+    assert bad.size == 0, f"{op}: {bad.size} mismatches, first x={x[bad[0]]!r} host={h[bad[0]]!r} dev={d[bad[0]]!r}"
+
+
+def _run_pair(p, steps, nbmode=O.NB_BRUTE, init_state=None):
+    o = O.Oracle(p, rng_mode=O.RNG_KEYED, nbmode=nbmode)
+    if init_state is None:
+        o.init_placement()
+        st = o.get_state()
+    else:
+        st = init_state
+        o.set_state(st)
+    sim = engine.Simulation(p)
+    sim.set_state(st)
+    assert sim.get_state().equal(st)
+    return o, sim
+
+
+def _compare_stepwise(p, steps, nbmode=O.NB_BRUTE, init_state=None):
+    o, sim = _run_pair(p, steps, nbmode, init_state)
+    obs_o, hashes = o.step(steps)
+    for s in range(steps):
+        rec = sim.step(1)
+        hs = sim.get_state()
+        h = engine.state_hash(p, hs)
+        if h != int(hashes[s]) or rec[0] != obs_o[s]:
+            o2, _ = _run_pair(p, 0, nbmode, init_state)
+            o2.step(s + 1, want_hashes=False)
+            ref = o2.get_state()
+            diff = [(name, np.argwhere(getattr(hs, name) != getattr(ref, name))[:5].tolist())
+                    for name in ("ra", "rb", "a_int", "b_int") if not np.array_equal(getattr(hs, name), getattr(ref, name))]
+            pytest.fail(f"step {s + 1}: hash {h:x} != {int(hashes[s]):x}; obs gpu={rec[0]} oracle={obs_o[s]}; "
+                        f"counters {hs.counters} vs {ref.counters}; diff {diff}")
+    sim.close()
+    return o
+
+
+def test_default_box_200_steps():
+    p = params(seed=11)
+    _compare_stepwise(p, 200)
+
+
+def test_dense_reactions_3000_steps():
+    p = params(seed=5, **DENSE)
+    o = _compare_stepwise(p, 3000)
+    st = o.stats()
+    assert st["rl"] > 0 and st["complex"] > 0 and st["laydown"] > 0
+
+
+def test_chunked_steps_equal_single_steps():
+    p = params(seed=3, **DENSE)
+    o = O.Oracle(p)
+    o.init_placement()
+    st = o.get_state()
+    sim = engine.Simulation(p)
+    sim.set_state(st)
+    obs = sim.step(1500)
+    obs_o, _ = o.step(1500, want_hashes=False)
+    assert np.array_equal(obs, obs_o)
+    assert engine.state_hash(p, sim.get_state()) == o.hash()
+
+
+def test_larger_box_cell_oracle():
+    # 4000 + 1500 at the dense area density; oracle with its cell list
+    p = params(n_a=4000, n_b=1500, seed=9, box_x=5200.0, box_y=5200.0, box_z=250.0,
+               **{k: v for k, v in DENSE.items() if not k.startswith("box")})
+    o = O.Oracle(p, nbmode=O.NB_CELLS)
+    o.init_placement()
+    st = o.get_state()
+    sim = engine.Simulation(p)
+    sim.set_state(st)
+    obs = sim.step(300)
+    obs_o, _ = o.step(300, want_hashes=False)
+    assert np.array_equal(obs, obs_o)
+    assert engine.state_hash(p, sim.get_state()) == o.hash()
