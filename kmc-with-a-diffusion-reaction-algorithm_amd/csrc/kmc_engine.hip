@@ -32,6 +32,7 @@ struct kmc_sim {
   Ctl* ctl_host = nullptr;
   // timing
   bool timing = false;
+  bool poison = false;
   double phase_ms[8] = {0};
   hipEvent_t ev[9] = {};
 };
@@ -203,6 +204,8 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   for (auto& e : s->ev) (void)hipEventCreate(&e);
   const char* tm = getenv("KMC_TIMING");
   s->timing = tm && *tm == '1';
+  const char* po = getenv("KMC_DEBUG_POISON");
+  s->poison = po && *po == '1';
   *out = s;
   return KMC_OK;
 }
@@ -318,6 +321,11 @@ static int launch_step(kmc_sim* s) {
     if (s->timing) (void)hipEventRecord(s->ev[i], st);
   };
   mark(0);
+  if (s->poison) {
+    // debug: every bead of R_new must be rewritten by a proposal or a revert
+    (void)hipMemsetAsync(d.nxt.a, 0xff, sizeof(double) * 48 * (size_t)K.NA, st);
+    (void)hipMemsetAsync(d.nxt.b, 0xff, sizeof(double) * 24 * (size_t)K.NB, st);
+  }
   k_begin<<<1, 1, 0, st>>>(d);
   k_classify<<<gN, T, 0, st>>>(K, d);
   if (K.NB > 0) {
@@ -326,7 +334,7 @@ static int launch_step(kmc_sim* s) {
   }
   mark(1);
   k_propose<<<gN, T, 0, st>>>(K, d);
-  if (K.NB > 0) k_complex<<<gB, 64, 0, st>>>(K, d);
+  if (K.NB > 0) k_complex<<<(K.NB + 63) / 64, 64, 0, st>>>(K, d);
   mark(2);
   k_rec_count<<<gN, T, 0, st>>>(K, d);
   k_scan1<<<s->nscan_blocks, SCAN_T, 0, st>>>(d.cell_cnt, d.cell_start, d.block_sums, s->ncell);

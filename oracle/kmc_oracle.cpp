@@ -202,7 +202,7 @@ struct Oracle {
         double d2 = dx * dx + dy * dy;
         double lim;
         if (p <= NA) lim = (k == 1 || k == 4) ? 0.3 : 20.3;
-        else lim = (j == 1) ? 0.3 : (k == 1 ? 35.0 : 65.0);
+        else lim = (j == 1) ? (k == 1 ? 0.3 : 30.3) : (k == 1 ? 35.0 : 65.0);
         if (!(d2 <= lim * lim))
           throw Err(KMC_ERR_GEOMETRY, "protein " + std::to_string(p) + " exceeds cell-list extent bound");
       }

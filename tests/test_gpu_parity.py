@@ -76,6 +76,22 @@ def test_dense_reactions_3000_steps():
     assert st["rl"] > 0 and st["complex"] > 0 and st["laydown"] > 0
 
 
+def test_poisoned_rnew_dense(monkeypatch):
+    # R_new filled with NaN before every step: any bead a proposal kernel
+    # forgets to write would surface as a mismatch
+    monkeypatch.setenv("KMC_DEBUG_POISON", "1")
+    p = params(seed=21, **DENSE)
+    o = O.Oracle(p)
+    o.init_placement()
+    st = o.get_state()
+    sim = engine.Simulation(p)
+    sim.set_state(st)
+    obs = sim.step(1000)
+    obs_o, _ = o.step(1000, want_hashes=False)
+    assert np.array_equal(obs, obs_o)
+    assert engine.state_hash(p, sim.get_state()) == o.hash()
+
+
 def test_chunked_steps_equal_single_steps():
     p = params(seed=3, **DENSE)
     o = O.Oracle(p)
@@ -89,16 +105,21 @@ def test_chunked_steps_equal_single_steps():
     assert engine.state_hash(p, sim.get_state()) == o.hash()
 
 
-def test_larger_box_cell_oracle():
-    # 4000 + 1500 at the dense area density; oracle with its cell list
-    p = params(n_a=4000, n_b=1500, seed=9, box_x=5200.0, box_y=5200.0, box_z=250.0,
-               **{k: v for k, v in DENSE.items() if not k.startswith("box")})
+RATES = {k: v for k, v in DENSE.items() if not k.startswith("box")}
+
+
+@pytest.mark.parametrize("n_a,n_b,L,steps", [(4000, 1500, 6000.0, 300), (20000, 7000, 14000.0, 150)])
+def test_larger_box_cell_oracle(n_a, n_b, L, steps):
+    # near the dense scenario's area density; the host generator's placement
+    # (proven identical to the oracle's, tests/test_host.py) and the oracle's
+    # cell list keep the CPU side tractable
+    p = params(n_a=n_a, n_b=n_b, seed=9, box_x=L, box_y=L, box_z=250.0, **RATES)
+    st = engine.host_init_random(p)
     o = O.Oracle(p, nbmode=O.NB_CELLS)
-    o.init_placement()
-    st = o.get_state()
+    o.set_state(st)
     sim = engine.Simulation(p)
     sim.set_state(st)
-    obs = sim.step(300)
-    obs_o, _ = o.step(300, want_hashes=False)
+    obs = sim.step(steps)
+    obs_o, _ = o.step(steps, want_hashes=False)
     assert np.array_equal(obs, obs_o)
     assert engine.state_hash(p, sim.get_state()) == o.hash()
