@@ -1296,6 +1296,19 @@ int64_t oracle_current_step(oracle_t* h) { return h->o->step_done; }
 // rng stream clock (stream mode), for tests that chain runs
 uint64_t oracle_stream_clock(oracle_t* h) { return h->o->rng.t; }
 uint64_t oracle_rand_calls(oracle_t* h) { return h->o->rng.grand.calls; }
+// known-answer hooks for the shared numerics headers (tests only)
+void oracle_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+  kmcr::u4 c{ctr[0], ctr[1], ctr[2], ctr[3]};
+  kmcr::u4 r = kmcr::philox4x32_10(c, key[0], key[1]);
+  out[0] = r.x;
+  out[1] = r.y;
+  out[2] = r.z;
+  out[3] = r.w;
+}
+void oracle_glibc_rand(uint32_t seed, int n, int32_t* out) {
+  kmcg::GlibcRand g(seed);
+  for (int i = 0; i < n; ++i) out[i] = g.next();
+}
 // resume the stream at clock t after `rand_calls` rand() calls
 void oracle_set_stream(oracle_t* h, uint64_t t, uint64_t rand_calls) {
   h->o->rng.t = t;
