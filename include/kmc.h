@@ -132,9 +132,15 @@ int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out);
 /* Last completed step number. */
 int64_t kmc_current_step(const kmc_sim* s);
 
-/* Device time of the most recent kmc_step call's per-phase kernels, for the
- * benchmark's roofline accounting (ms, summed over the call). */
-int kmc_phase_times(const kmc_sim* s, double* ms_out, int32_t n);
+/* Per-kernel device time, measured with HIP events on the handle's stream:
+ * kmc_set_timing(s, mask) brackets every launch of the kernels whose id bit
+ * is set (ids: kmc_kernel_name(0..n-1); 0 disables and resets), and
+ * kmc_kernel_times returns the accumulated milliseconds and launch counts
+ * since; both return the number of kernel ids.  Used by bench.py for the
+ * roofline of the dominant kernel. */
+int kmc_set_timing(kmc_sim* s, uint64_t kernel_mask);
+int kmc_kernel_times(const kmc_sim* s, double* total_ms, int64_t* launches, int32_t n);
+const char* kmc_kernel_name(int32_t id);
 
 /* Formatting helpers shared by every host driver.  Each returns the number of
  * characters written (excluding NUL) or < 0. */

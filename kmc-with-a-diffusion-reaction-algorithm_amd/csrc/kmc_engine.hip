@@ -16,6 +16,18 @@
 
 using namespace kmcd;
 
+// kernel ids for per-kernel HIP-event timing (kmc_set_timing / kmc_kernel_times)
+enum KId {
+  KI_BEGIN, KI_CLASSIFY, KI_BFS, KI_BFS_OVF, KI_PROPOSE, KI_COMPLEX, KI_REC_COUNT, KI_SCAN, KI_REC_SCATTER,
+  KI_RESOLVE0, KI_RESOLVE1, KI_RESOLVE_TAIL, KI_COMMIT, KI_RXN_CAND, KI_RL_MATCH, KI_CIS_MATCH, KI_DISS_RL,
+  KI_DISS_CIS, KI_OBSERVE, KI_FINALIZE, KI_N
+};
+static const char* const KNAMES[KI_N] = {
+    "k_begin", "k_classify", "k_bfs", "k_bfs_overflow", "k_propose", "k_complex", "k_rec_count", "k_scan",
+    "k_rec_scatter", "k_resolve_r0", "k_resolve_r1", "k_resolve_tail", "k_commit", "k_rxn_candidates",
+    "k_rl_match", "k_cis_match", "k_diss_rl", "k_diss_cis", "k_observe", "k_finalize"};
+#define TRING 64  // steps of event pairs kept in flight
+
 struct kmc_sim {
   kmc_params p;
   KParams K;
@@ -30,11 +42,14 @@ struct kmc_sim {
   kmc_obs_dev* obs_buf = nullptr;
   int64_t obs_cap = 0;
   Ctl* ctl_host = nullptr;
-  // timing
-  bool timing = false;
   bool poison = false;
-  double phase_ms[8] = {0};
-  hipEvent_t ev[9] = {};
+  // per-kernel timing: a ring of TRING steps of event pairs, read back lazily
+  uint64_t tmask = 0;
+  std::vector<hipEvent_t> tev;  // [TRING][KI_N][2]
+  std::vector<uint8_t> tused;   // [TRING][KI_N]
+  int tslot = 0;
+  double kms[KI_N] = {0};
+  int64_t kcount[KI_N] = {0};
 };
 
 namespace {
@@ -201,9 +216,6 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
     kmc_destroy(s);
     return KMC_ERR_HIP;
   }
-  for (auto& e : s->ev) (void)hipEventCreate(&e);
-  const char* tm = getenv("KMC_TIMING");
-  s->timing = tm && *tm == '1';
   const char* po = getenv("KMC_DEBUG_POISON");
   s->poison = po && *po == '1';
   *out = s;
@@ -216,7 +228,7 @@ int kmc_destroy(kmc_sim* s) {
   for (void* v : s->allocs) (void)hipFree(v);
   if (s->obs_buf) (void)hipFree(s->obs_buf);
   if (s->ctl_host) (void)hipHostFree(s->ctl_host);
-  for (auto& e : s->ev)
+  for (auto& e : s->tev)
     if (e) (void)hipEventDestroy(e);
   if (s->stream) (void)hipStreamDestroy(s->stream);
   delete s;
@@ -311,53 +323,82 @@ int kmc_write_cpt(kmc_sim* s, const char* path) {
   return kmch_host::write_cpt(&s->p, &v, path, &s->err);
 }
 
+// accumulate the event pairs of ring slot `slot` (already complete or waited on)
+static void harvest(kmc_sim* s, int slot) {
+  for (int k = 0; k < KI_N; ++k) {
+    size_t i = (size_t)slot * KI_N + k;
+    if (!s->tused[i]) continue;
+    float ms = 0;
+    (void)hipEventSynchronize(s->tev[2 * i + 1]);
+    if (hipEventElapsedTime(&ms, s->tev[2 * i], s->tev[2 * i + 1]) == hipSuccess) {
+      s->kms[k] += ms;
+      s->kcount[k] += 1;
+    }
+    s->tused[i] = 0;
+  }
+}
+
+struct Bracket {
+  kmc_sim* s;
+  int k;
+  Bracket(kmc_sim* s_, int k_) : s(s_), k(k_) {
+    if (s->tmask >> k & 1) (void)hipEventRecord(s->tev[2 * ((size_t)s->tslot * KI_N + k)], s->stream);
+  }
+  ~Bracket() {
+    if (s->tmask >> k & 1) {
+      size_t i = (size_t)s->tslot * KI_N + k;
+      (void)hipEventRecord(s->tev[2 * i + 1], s->stream);
+      s->tused[i] = 1;
+    }
+  }
+};
+#define TIMED(k, ...) \
+  do {                \
+    Bracket b_(s, k); \
+    __VA_ARGS__;      \
+  } while (0)
+
 static int launch_step(kmc_sim* s) {
   const KParams& K = s->K;
   Dev& d = s->d;
   hipStream_t st = s->stream;
   const int T = 256;
   const int gN = (K.N + T - 1) / T, gA = (K.NA + T - 1) / T, gB = (K.NB + T - 1) / T;
-  auto mark = [&](int i) {
-    if (s->timing) (void)hipEventRecord(s->ev[i], st);
-  };
-  mark(0);
+  if (s->tmask) harvest(s, s->tslot);  // the slot's previous use is TRING steps old
   if (s->poison) {
     // debug: every bead of R_new must be rewritten by a proposal or a revert
     (void)hipMemsetAsync(d.nxt.a, 0xff, sizeof(double) * 48 * (size_t)K.NA, st);
     (void)hipMemsetAsync(d.nxt.b, 0xff, sizeof(double) * 24 * (size_t)K.NB, st);
   }
-  k_begin<<<1, 1, 0, st>>>(d);
-  k_classify<<<gN, T, 0, st>>>(K, d);
+  TIMED(KI_BEGIN, (k_begin<<<1, 1, 0, st>>>(d)));
+  TIMED(KI_CLASSIFY, (k_classify<<<gN, T, 0, st>>>(K, d)));
   if (K.NB > 0) {
-    k_bfs<<<gB, T, 0, st>>>(K, d);
-    k_bfs_overflow<<<1, 64, 0, st>>>(K, d);
+    TIMED(KI_BFS, (k_bfs<<<gB, T, 0, st>>>(K, d)));
+    TIMED(KI_BFS_OVF, (k_bfs_overflow<<<1, 64, 0, st>>>(K, d)));
   }
-  mark(1);
-  k_propose<<<gN, T, 0, st>>>(K, d);
-  if (K.NB > 0) k_complex<<<(K.NB + 63) / 64, 64, 0, st>>>(K, d);
-  mark(2);
-  k_rec_count<<<gN, T, 0, st>>>(K, d);
-  k_scan1<<<s->nscan_blocks, SCAN_T, 0, st>>>(d.cell_cnt, d.cell_start, d.block_sums, s->ncell);
-  k_scan2<<<1, SCAN_T, 0, st>>>(d.block_sums, s->nscan_blocks, d.cell_start + s->ncell);
-  k_scan3<<<s->nscan_blocks, SCAN_T, 0, st>>>(d.cell_start, d.block_sums, s->ncell);
-  k_rec_scatter<<<gN, T, 0, st>>>(K, d);
-  mark(3);
-  k_resolve<<<gN, T, 0, st>>>(K, d, -1);
-  k_resolve<<<gN, T, 0, st>>>(K, d, 0);
-  k_resolve_tail<<<1, 1024, 0, st>>>(K, d);
-  k_commit<<<gN, T, 0, st>>>(K, d);
-  mark(4);
+  TIMED(KI_PROPOSE, (k_propose<<<gN, T, 0, st>>>(K, d)));
+  if (K.NB > 0) TIMED(KI_COMPLEX, (k_complex<<<(K.NB + 63) / 64, 64, 0, st>>>(K, d)));
+  TIMED(KI_REC_COUNT, (k_rec_count<<<gN, T, 0, st>>>(K, d)));
+  TIMED(KI_SCAN, {
+    k_scan1<<<s->nscan_blocks, SCAN_T, 0, st>>>(d.cell_cnt, d.cell_start, d.block_sums, s->ncell);
+    k_scan2<<<1, SCAN_T, 0, st>>>(d.block_sums, s->nscan_blocks, d.cell_start + s->ncell);
+    k_scan3<<<s->nscan_blocks, SCAN_T, 0, st>>>(d.cell_start, d.block_sums, s->ncell);
+  });
+  TIMED(KI_REC_SCATTER, (k_rec_scatter<<<gN, T, 0, st>>>(K, d)));
+  TIMED(KI_RESOLVE0, (k_resolve<<<gN, T, 0, st>>>(K, d, -1)));
+  TIMED(KI_RESOLVE1, (k_resolve<<<gN, T, 0, st>>>(K, d, 0)));
+  TIMED(KI_RESOLVE_TAIL, (k_resolve_tail<<<1, 1024, 0, st>>>(K, d)));
+  TIMED(KI_COMMIT, (k_commit<<<gN, T, 0, st>>>(K, d)));
   if (K.NA > 0) {
-    k_rxn_candidates<<<gA, T, 0, st>>>(K, d);
-    k_rl_match<<<1, 1024, 0, st>>>(K, d);
-    k_cis_match<<<1, 1024, 0, st>>>(K, d);
-    k_diss_rl<<<gA, T, 0, st>>>(K, d);
-    k_diss_cis<<<gA, T, 0, st>>>(K, d);
+    TIMED(KI_RXN_CAND, (k_rxn_candidates<<<gA, T, 0, st>>>(K, d)));
+    TIMED(KI_RL_MATCH, (k_rl_match<<<1, 1024, 0, st>>>(K, d)));
+    TIMED(KI_CIS_MATCH, (k_cis_match<<<1, 1024, 0, st>>>(K, d)));
+    TIMED(KI_DISS_RL, (k_diss_rl<<<gA, T, 0, st>>>(K, d)));
+    TIMED(KI_DISS_CIS, (k_diss_cis<<<gA, T, 0, st>>>(K, d)));
   }
-  mark(5);
-  k_observe<<<gN, T, 0, st>>>(K, d);
-  k_finalize<<<1, 1, 0, st>>>(K, d, s->p.time_step);
-  mark(6);
+  TIMED(KI_OBSERVE, (k_observe<<<gN, T, 0, st>>>(K, d)));
+  TIMED(KI_FINALIZE, (k_finalize<<<1, 1, 0, st>>>(K, d, s->p.time_step)));
+  if (s->tmask) s->tslot = (s->tslot + 1) % TRING;
   // R_new becomes R (main.cpp:2164-2191): swap the bead buffers
   std::swap(d.cur, d.nxt);
   return KMC_OK;
@@ -374,28 +415,19 @@ int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out) {
     s->obs_cap = chunk;
     s->d.obs = s->obs_buf;
   }
-  for (int i = 0; i < 8; ++i) s->phase_ms[i] = 0;
   int64_t done = 0;
   while (done < nsteps) {
     int64_t n = std::min(chunk, nsteps - done);
     uint32_t zero = 0;
     HIPCHK(s, hipMemcpyAsync(&s->d.ctl->obs_idx, &zero, sizeof zero, hipMemcpyHostToDevice, s->stream));
-    for (int64_t k = 0; k < n; ++k) {
-      launch_step(s);
-      if (s->timing) {
-        (void)hipEventSynchronize(s->ev[6]);
-        for (int i = 0; i < 6; ++i) {
-          float ms = 0;
-          (void)hipEventElapsedTime(&ms, s->ev[i], s->ev[i + 1]);
-          s->phase_ms[i] += ms;
-        }
-      }
-    }
+    for (int64_t k = 0; k < n; ++k) launch_step(s);
     HIPCHK(s, hipGetLastError());
     HIPCHK(s, hipMemcpyAsync(s->ctl_host, s->d.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, s->stream));
     if (out)
       HIPCHK(s, hipMemcpyAsync(out + done, s->obs_buf, sizeof(kmc_obs_dev) * n, hipMemcpyDeviceToHost, s->stream));
     HIPCHK(s, hipStreamSynchronize(s->stream));
+    if (s->tmask)
+      for (int slot = 0; slot < TRING; ++slot) harvest(s, slot);
     s->step_done += n;
     uint32_t err = s->ctl_host->err;
     if (err) {
@@ -447,10 +479,30 @@ int kmc_device_math(int op, const double* x, const double* y, double* out, int64
   return rc;
 }
 
-int kmc_phase_times(const kmc_sim* s, double* ms_out, int32_t n) {
-  if (!s || !ms_out) return KMC_ERR_ARG;
-  for (int i = 0; i < n && i < 8; ++i) ms_out[i] = s->phase_ms[i];
-  return 6;
+int kmc_set_timing(kmc_sim* s, uint64_t kernel_mask) {
+  if (!s) return KMC_ERR_ARG;
+  if (kernel_mask && s->tev.empty()) {
+    s->tev.assign((size_t)TRING * KI_N * 2, nullptr);
+    s->tused.assign((size_t)TRING * KI_N, 0);
+    for (auto& e : s->tev) HIPCHK(s, hipEventCreate(&e));
+  }
+  s->tmask = kernel_mask;
+  for (int k = 0; k < KI_N; ++k) {
+    s->kms[k] = 0;
+    s->kcount[k] = 0;
+  }
+  return KMC_OK;
 }
+
+int kmc_kernel_times(const kmc_sim* s, double* total_ms, int64_t* launches, int32_t n) {
+  if (!s) return KMC_ERR_ARG;
+  for (int k = 0; k < n && k < KI_N; ++k) {
+    if (total_ms) total_ms[k] = s->kms[k];
+    if (launches) launches[k] = s->kcount[k];
+  }
+  return KI_N;
+}
+
+const char* kmc_kernel_name(int32_t id) { return id >= 0 && id < KI_N ? KNAMES[id] : ""; }
 
 }  // extern "C"

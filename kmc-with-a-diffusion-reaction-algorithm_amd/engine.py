@@ -54,7 +54,10 @@ def load_library(path: Optional[str] = None):
     L.kmc_step.argtypes = [C.c_void_p, C.c_int64, C.c_void_p]
     L.kmc_current_step.restype = C.c_int64
     L.kmc_current_step.argtypes = [C.c_void_p]
-    L.kmc_phase_times.argtypes = [C.c_void_p, P(C.c_double), C.c_int32]
+    L.kmc_set_timing.argtypes = [C.c_void_p, C.c_uint64]
+    L.kmc_kernel_times.argtypes = [C.c_void_p, P(C.c_double), P(C.c_int64), C.c_int32]
+    L.kmc_kernel_name.restype = C.c_char_p
+    L.kmc_kernel_name.argtypes = [C.c_int32]
     L.kmc_format_bond_line.argtypes = [P(capi.Params), P(capi.Obs), C.c_char_p, C.c_size_t]
     L.kmc_state_hash.restype = C.c_uint64
     L.kmc_state_hash.argtypes = [P(capi.Params), P(capi.StateView)]
@@ -197,7 +200,30 @@ class Simulation:
     def current_step(self) -> int:
         return int(load_library().kmc_current_step(self._h))
 
-    def phase_times(self) -> np.ndarray:
-        buf = (C.c_double * 8)()
-        n = load_library().kmc_phase_times(self._h, buf, 8)
-        return np.array(buf[:n])
+    def set_timing(self, kernels=()):
+        """Bracket the named kernels with HIP events (empty: off)."""
+        names = kernel_names()
+        mask = 0
+        for k in kernels:
+            mask |= 1 << names.index(k)
+        self._check(load_library().kmc_set_timing(self._h, mask))
+
+    def kernel_times(self) -> dict:
+        """{kernel: (total_ms, launches)} accumulated since set_timing."""
+        ms = (C.c_double * 64)()
+        cnt = (C.c_int64 * 64)()
+        n = load_library().kmc_kernel_times(self._h, ms, cnt, 64)
+        names = kernel_names()
+        return {names[i]: (ms[i], cnt[i]) for i in range(n) if cnt[i]}
+
+
+def kernel_names():
+    L = load_library()
+    out = []
+    i = 0
+    while True:
+        nm = L.kmc_kernel_name(i).decode()
+        if not nm:
+            return out
+        out.append(nm)
+        i += 1
