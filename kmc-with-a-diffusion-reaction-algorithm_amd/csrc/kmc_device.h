@@ -43,7 +43,7 @@ struct Ctl {
   uint32_t n_wl[2];       // resolution work lists
   uint32_t n_rl;          // R–L accepting edges
   uint32_t n_cisc;        // cis candidates
-  uint32_t pad1;
+  uint32_t n_pairs;       // reaction (receptor, record) pairs
   // observables (reduced per step)
   int32_t rl, mono, cis;  // derived from state
   int32_t tot_prot, tot_clu, max_size;

@@ -18,13 +18,13 @@ using namespace kmcd;
 
 // kernel ids for per-kernel HIP-event timing (kmc_set_timing / kmc_kernel_times)
 enum KId {
-  KI_BEGIN, KI_CLASSIFY, KI_BFS, KI_BFS_OVF, KI_PROPOSE, KI_COMPLEX, KI_REC_COUNT, KI_SCAN, KI_REC_SCATTER,
-  KI_RESOLVE0, KI_RESOLVE1, KI_RESOLVE_TAIL, KI_COMMIT, KI_RXN_CAND, KI_RL_MATCH, KI_CIS_MATCH, KI_DISS_RL,
+  KI_CLASSIFY, KI_BFS, KI_BFS_OVF, KI_PROPOSE, KI_COMPLEX, KI_REC_COUNT, KI_SCAN, KI_REC_SCATTER,
+  KI_RESOLVE0, KI_RESOLVE1, KI_RESOLVE_TAIL, KI_COMMIT, KI_RXN_SCAN, KI_RXN_EXACT, KI_RL_MATCH, KI_CIS_MATCH, KI_DISS_RL,
   KI_DISS_CIS, KI_OBSERVE, KI_FINALIZE, KI_N
 };
 static const char* const KNAMES[KI_N] = {
-    "k_begin", "k_classify", "k_bfs", "k_bfs_overflow", "k_propose", "k_complex", "k_rec_count", "k_scan",
-    "k_rec_scatter", "k_resolve_r0", "k_resolve_r1", "k_resolve_tail", "k_commit", "k_rxn_candidates",
+    "k_classify", "k_bfs", "k_bfs_overflow", "k_propose", "k_complex", "k_rec_count", "k_scan",
+    "k_rec_scatter", "k_resolve_r0", "k_resolve_r1", "k_resolve_tail", "k_commit", "k_rxn_scan", "k_rxn_exact",
     "k_rl_match", "k_cis_match", "k_diss_rl", "k_diss_cis", "k_observe", "k_finalize"};
 #define TRING 64  // steps of event pairs kept in flight
 
@@ -201,6 +201,9 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   rc |= dalloc(s, &d.block_sums, s->nscan_blocks);
   rc |= dalloc(s, &d.rec_pos, (size_t)2 * N);
   rc |= dalloc(s, &d.rec_id, (size_t)2 * N);
+  d.cap_pairs = pow2(std::max<uint32_t>(1u << 16, (uint32_t)N));
+  rc |= dalloc(s, &d.pairs, d.cap_pairs);
+  rc |= dalloc(s, &d.rfinal, N);
   rc |= dalloc(s, &d.rl_keys, cap);
   rc |= dalloc(s, &d.cis_keys, cap);
   rc |= dalloc(s, &d.ent, (size_t)2 * cap);
@@ -370,7 +373,6 @@ static int launch_step(kmc_sim* s) {
     (void)hipMemsetAsync(d.nxt.a, 0xff, sizeof(double) * 48 * (size_t)K.NA, st);
     (void)hipMemsetAsync(d.nxt.b, 0xff, sizeof(double) * 24 * (size_t)K.NB, st);
   }
-  TIMED(KI_BEGIN, (k_begin<<<1, 1, 0, st>>>(d)));
   TIMED(KI_CLASSIFY, (k_classify<<<gN, T, 0, st>>>(K, d)));
   if (K.NB > 0) {
     TIMED(KI_BFS, (k_bfs<<<gB, T, 0, st>>>(K, d)));
@@ -385,12 +387,14 @@ static int launch_step(kmc_sim* s) {
     k_scan3<<<s->nscan_blocks, SCAN_T, 0, st>>>(d.cell_start, d.block_sums, s->ncell);
   });
   TIMED(KI_REC_SCATTER, (k_rec_scatter<<<gN, T, 0, st>>>(K, d)));
-  TIMED(KI_RESOLVE0, (k_resolve<<<gN, T, 0, st>>>(K, d, -1)));
+  const int gR = (2 * K.N + T - 1) / T;
+  TIMED(KI_RESOLVE0, (k_resolve0<<<gR, T, 0, st>>>(K, d)));
   TIMED(KI_RESOLVE1, (k_resolve<<<gN, T, 0, st>>>(K, d, 0)));
   TIMED(KI_RESOLVE_TAIL, (k_resolve_tail<<<1, 1024, 0, st>>>(K, d)));
   TIMED(KI_COMMIT, (k_commit<<<gN, T, 0, st>>>(K, d)));
   if (K.NA > 0) {
-    TIMED(KI_RXN_CAND, (k_rxn_candidates<<<gA, T, 0, st>>>(K, d)));
+    TIMED(KI_RXN_SCAN, (k_rxn_scan<<<gR, T, 0, st>>>(K, d)));
+    TIMED(KI_RXN_EXACT, (k_rxn_exact<<<1024, T, 0, st>>>(K, d)));
     TIMED(KI_RL_MATCH, (k_rl_match<<<1, 1024, 0, st>>>(K, d)));
     TIMED(KI_CIS_MATCH, (k_cis_match<<<1, 1024, 0, st>>>(K, d)));
     TIMED(KI_DISS_RL, (k_diss_rl<<<gA, T, 0, st>>>(K, d)));

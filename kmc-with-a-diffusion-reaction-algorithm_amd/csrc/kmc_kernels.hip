@@ -49,7 +49,10 @@ struct Dev {
   int32_t* cell_start;  // [ncell+1]
   int32_t* block_sums;  // [scan blocks]
   float4* rec_pos;      // [2N]
-  int32_t* rec_id;      // [2N]  pid | isnew<<31
+  int2* rec_id;         // [2N]  {pid | isnew<<31, owner key}
+  int2* pairs;          // [cap_pairs] reaction candidate (receptor, record)
+  uint8_t* rfinal;      // [N] 1 if the proposal record is the final position
+  uint32_t cap_pairs;
   uint64_t* rl_keys;    // [cap]
   uint64_t* cis_keys;   // [cap]
   uint64_t* ent;        // [2*cap] greedy scratch
@@ -142,10 +145,6 @@ __global__ void k_classify(KParams P, Dev d) {
   }
   d.ukind[p] = kind;
   d.owner[p] = own;  // -1: complex member, set by the BFS kernels
-  if (kind != U_NONE) {
-    uint32_t s = atomicAdd(&d.ctl->n_units, 1u);
-    d.units[s] = p;
-  }
 }
 
 // ================================================================ BFS
@@ -191,8 +190,6 @@ __device__ void register_complex(const KParams& P, const Dev& d, int p, const in
   d.cx_size[b] = qn;
   d.cx_nb[b] = nb;
   d.ukind[p] = U_COMPLEX;
-  uint32_t s = atomicAdd(&d.ctl->n_units, 1u);
-  d.units[s] = p;
   (void)global_q;
 }
 
@@ -792,8 +789,9 @@ __device__ __forceinline__ void ref_point(const Dev& d, const Beads& B, int p, i
   if (p < NA) {
     x = B.A(p, 1, 1, 0);
     y = B.A(p, 1, 1, 1);
-    zlo = B.A(p, 1, 1, 2);
-    zhi = B.A(p, 4, 1, 2);
+    double z1 = B.A(p, 1, 1, 2), z2 = B.A(p, 2, 1, 2), z3 = B.A(p, 3, 1, 2), z4 = B.A(p, 4, 1, 2);
+    zlo = fmin(fmin(z1, z2), fmin(z3, z4));  // the axis span of the four domains
+    zhi = fmax(fmax(z1, z2), fmax(z3, z4));
   } else {
     x = B.B(p - NA, 1, 1, 0);
     y = B.B(p - NA, 1, 1, 1);
@@ -890,16 +888,22 @@ __global__ void k_scan3(int32_t* out, const int32_t* sums, int n) {
     if (base + q < n) out[base + q] += add;
 }
 
+#define RID_PID 0x00ffffff
+#define RID_ST3 (1 << 29)
+#define RID_ST2 (1 << 30)
 __global__ void k_rec_scatter(KParams P, Dev d) {
+  const int NA = P.NA;
   int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P.N) return;
+  int st = 0;
+  if (p < NA) st = (A_ST2(d, p) ? RID_ST2 : 0) | (A_ST3(d, p) ? RID_ST3 : 0);
   for (int w = 0; w < 2; ++w) {
     double x, y, zl, zh;
     ref_point(d, w ? d.nxt : d.cur, p, P.NA, x, y, zl, zh);
     int c = cell_y(P, y) * P.ncx + cell_x(P, x);
     int pos = d.cell_start[c] + atomicSub(&d.cell_cnt[c], 1) - 1;  // leaves cell_cnt zeroed
     d.rec_pos[pos] = make_float4((float)x, (float)y, (float)zl, (float)zh);
-    d.rec_id[pos] = p | (w << 31);
+    d.rec_id[pos] = make_int2(p | st | (w << 31), d.owner[p]);
   }
 }
 
@@ -997,7 +1001,7 @@ __device__ __forceinline__ bool prefilter(bool mA, float mx, float my, float mzl
   return lz > alo - 86.5f && lz < ahi + 86.5f;
 }
 
-__device__ uint32_t evaluate_unit(const KParams& P, const Dev& d, int u, uint32_t step) {
+__device__ uint32_t evaluate_unit(const KParams& P, const Dev& d, int u, uint32_t step, const float4* key_ref) {
   const int NA = P.NA;
   uint8_t kind = d.ukind[u];
   int nm;
@@ -1020,21 +1024,38 @@ __device__ uint32_t evaluate_unit(const KParams& P, const Dev& d, int u, uint32_
   bool blocked = false;
   for (int t = 0; t < nm; ++t) {
     int m = mem[t];
+    const bool mA = m < NA;
+    float mx, my, mzl, mzh;
+    if (key_ref && m == u) {
+      mx = key_ref->x;
+      my = key_ref->y;
+      mzl = key_ref->z;
+      mzh = key_ref->w;
+    } else {
+      double x, y, zl, zh;
+      ref_point(d, d.nxt, m, NA, x, y, zl, zh);
+      mx = (float)x;
+      my = (float)y;
+      mzl = (float)zl;
+      mzh = (float)zh;
+    }
+    // cell of the proposal: from the exact [1][1] (records are binned on it)
+    double ex = mA ? d.nxt.A(m, 1, 1, 0) : d.nxt.B(m - NA, 1, 1, 0);
+    double ey = mA ? d.nxt.A(m, 1, 1, 1) : d.nxt.B(m - NA, 1, 1, 1);
+    int cx = cell_x(P, ex), cy = cell_y(P, ey);
     Own o;
-    load_own(P, d.nxt, m, o);
-    float mx = (float)o.x[0], my = (float)o.y[0], mzl = (float)o.z[0];
-    float mzh = o.isA ? (float)o.z[3] : mzl;
-    int cx = cell_x(P, o.x[0]), cy = cell_y(P, o.y[0]);
+    bool loaded = false;
     for (int yy = cy - 1; yy <= cy + 1; ++yy) {
       if (yy < 0 || yy >= P.ncy) continue;
       int x0 = cx > 0 ? cx - 1 : 0, x1 = cx + 1 < P.ncx ? cx + 1 : P.ncx - 1;
       int r0 = d.cell_start[yy * P.ncx + x0], r1 = d.cell_start[yy * P.ncx + x1 + 1];
       for (int r = r0; r < r1; ++r) {
-        int id = d.rec_id[r];
-        int q = id & 0x7fffffff;
-        bool isnew = id < 0;
+        int2 id = d.rec_id[r];
+        int q = id.x & RID_PID;
         if (q == m) continue;
-        int kq = d.owner[q];
+        if (!prefilter(mA, mx, my, mzl, mzh, q < NA, d.rec_pos[r])) continue;
+        bool isnew = id.x < 0;
+        int kq = id.y;
         bool pending = false;
         if (kq < 0) {
           atomicOr(&d.ctl->err, ERR_RESOLVE);
@@ -1045,16 +1066,19 @@ __device__ uint32_t evaluate_unit(const KParams& P, const Dev& d, int u, uint32_
         } else if (kq > u) {
           if (isnew) continue;
         } else {
-          uint32_t s = state_of(d, kq, step);
-          if (s == S_ACC) {
+          uint32_t st = state_of(d, kq, step);
+          if (st == S_ACC) {
             if (!isnew) continue;
-          } else if (s == S_REJ) {
+          } else if (st == S_REJ) {
             if (isnew) continue;
           } else {
             pending = true;
           }
         }
-        if (!prefilter(o.isA, mx, my, mzl, mzh, q < NA, d.rec_pos[r])) continue;
+        if (!loaded) {
+          load_own(P, d.nxt, m, o);
+          loaded = true;
+        }
         if (exact_collide(P, o, isnew ? d.nxt : d.cur, q)) {
           if (!pending) return S_REJ;
           blocked = true;
@@ -1065,15 +1089,37 @@ __device__ uint32_t evaluate_unit(const KParams& P, const Dev& d, int u, uint32_
   return blocked ? S_UND : S_ACC;
 }
 
+// round 0: one thread per record in cell order — the thread holding a unit
+// key's proposal record evaluates that unit, so a wave's lanes scan
+// neighbouring cells (spatially coherent loads)
+__global__ void k_resolve0(KParams P, Dev d) {
+  int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= 2 * P.N) return;
+  int2 id = d.rec_id[r];
+  if (id.x >= 0) return;  // old-position record
+  int u = id.x & RID_PID;
+  if (id.y != u || d.ukind[u] == U_NONE) return;
+  float4 ref = d.rec_pos[r];
+  const uint32_t step = d.ctl->step;
+  uint32_t s = evaluate_unit(P, d, u, step, &ref);
+  if (s == S_UND) {
+    uint32_t pos = atomicAdd(&d.ctl->n_wl[0], 1u);
+    d.wl0[pos] = u;
+  } else {
+    set_state(d, u, step, s);
+  }
+}
+
+// round 1: the units round 0 left undecided
 __global__ void k_resolve(KParams P, Dev d, int src) {
   const uint32_t step = d.ctl->step;
-  uint32_t n = src < 0 ? d.ctl->n_units : d.ctl->n_wl[src];
-  const int32_t* list = src < 0 ? d.units : (src == 0 ? d.wl0 : d.wl1);
-  int32_t* dst = src < 0 ? d.wl0 : d.wl1;
-  uint32_t* ndst = src < 0 ? &d.ctl->n_wl[0] : &d.ctl->n_wl[1];
+  uint32_t n = d.ctl->n_wl[src];
+  const int32_t* list = src == 0 ? d.wl0 : d.wl1;
+  int32_t* dst = src == 0 ? d.wl1 : d.wl0;
+  uint32_t* ndst = &d.ctl->n_wl[src ^ 1];
   for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
     int u = list[t];
-    uint32_t s = evaluate_unit(P, d, u, step);
+    uint32_t s = evaluate_unit(P, d, u, step, nullptr);
     if (s == S_UND) {
       uint32_t pos = atomicAdd(ndst, 1u);
       dst[pos] = u;
@@ -1102,7 +1148,7 @@ __global__ void __launch_bounds__(1024) k_resolve_tail(KParams P, Dev d) {
     int32_t* dst = flip ? d.wl1 : d.wl0;
     for (uint32_t t = threadIdx.x; t < n_cur; t += blockDim.x) {
       int u = src[t];
-      uint32_t s = evaluate_unit(P, d, u, step);
+      uint32_t s = evaluate_unit(P, d, u, step, nullptr);
       if (s == S_UND) dst[atomicAdd(&n_next, 1u)] = u;
       else set_state(d, u, step, s);
     }
@@ -1125,6 +1171,7 @@ __global__ void k_commit(KParams P, Dev d) {
   if (p >= P.N) return;
   const uint32_t step = d.ctl->step;
   uint32_t s = state_of(d, d.owner[p], step);
+  d.rfinal[p] = s == S_ACC;
   if (s == S_ACC) return;
   if (s != S_REJ) {
     atomicOr(&d.ctl->err, ERR_RESOLVE);
@@ -1139,87 +1186,121 @@ __global__ void k_commit(KParams P, Dev d) {
 }
 
 // ================================================================ 6. reactions
-__device__ __forceinline__ bool record_final(const Dev& d, int id, uint32_t step) {
-  int q = id & 0x7fffffff;
-  bool isnew = id < 0;
-  uint32_t s = state_of(d, d.owner[q], step);
-  return isnew ? s == S_ACC : s == S_REJ;
+__device__ __forceinline__ bool record_final(const Dev& d, int2 id) {
+  return (id.x < 0) == (d.rfinal[id.x & RID_PID] != 0);
 }
 
-// Candidate pairs (after diffusion, from R_new): R–L association gates
-// main.cpp:1880-1921 and cis gates 1954-1985 / 2009-2039.  A pair becomes an
-// accepting edge when its keyed draw is below the acceptance probability;
-// the greedy kernels below replay the reference's loop order on those edges.
-__global__ void k_rxn_candidates(KParams P, Dev d) {
+// Reaction candidates, pass 1: one thread per record in cell order; the
+// final-position record of a receptor that can still react scans the final
+// records of its 3x3 cells with conservative single-precision prefilters
+// (R–L: ligand centre within reach of the [3][2] site; cis: the two [3][3]
+// sites within 16 Å) and emits (receptor, partner) pairs.  Light on
+// registers; the exact gates run in pass 2 over the (few) pairs.
+__global__ void k_rxn_scan(KParams P, Dev d) {
   const int NA = P.NA, NB = P.NB;
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= 2 * P.N) return;
+  int2 me = d.rec_id[r];
+  int i = me.x & RID_PID;
   if (i >= NA) return;
-  const uint32_t step = d.ctl->step;
-  const Beads& N = d.nxt;
-  bool want_rl = A_ST2(d, i) == 0 && NB > 0;
-  bool want_cis = A_ST3(d, i) == 0;
+  bool want_rl = !(me.x & RID_ST2) && NB > 0;
+  bool want_cis = !(me.x & RID_ST3);
   if (!want_rl && !want_cis) return;
+  if (!record_final(d, me)) return;
+  const Beads& N = d.nxt;
+  float4 mp = d.rec_pos[r];
+  float fx = mp.x, fy = mp.y, fzl = mp.z, fzh = mp.w;
+  float sx = 0, sy = 0;
+  bool have_site = false;
   double ax = N.A(i, 1, 1, 0), ay = N.A(i, 1, 1, 1);
-  float fx = (float)ax, fy = (float)ay, fzl = (float)N.A(i, 1, 1, 2), fzh = (float)N.A(i, 4, 1, 2);
   int cx = cell_x(P, ax), cy = cell_y(P, ay);
   for (int yy = cy - 1; yy <= cy + 1; ++yy) {
     if (yy < 0 || yy >= P.ncy) continue;
     int x0 = cx > 0 ? cx - 1 : 0, x1 = cx + 1 < P.ncx ? cx + 1 : P.ncx - 1;
     int r0 = d.cell_start[yy * P.ncx + x0], r1 = d.cell_start[yy * P.ncx + x1 + 1];
-    for (int r = r0; r < r1; ++r) {
-      int id = d.rec_id[r];
-      int q = id & 0x7fffffff;
+    for (int rr = r0; rr < r1; ++rr) {
+      int2 id = d.rec_id[rr];
+      int q = id.x & RID_PID;
       if (q == i) continue;
-      float4 rp = d.rec_pos[r];
+      float4 rp = d.rec_pos[rr];
       float dx = rp.x - fx, dy = rp.y - fy;
       float dxy2 = dx * dx + dy * dy;
       if (q >= NA) {
         if (!want_rl) continue;
         if (!(dxy2 < 105.0f * 105.0f) || !(rp.z > fzl - 85.0f && rp.z < fzh + 85.0f)) continue;
-        if (!record_final(d, id, step)) continue;
-        int lb = q - NA;
-        for (int k = 2; k <= 4; ++k) {
-          if (B_ST(d, lb, k) != 0) continue;
-          double ddx = N.B(lb, k, 2, 0) - N.A(i, 3, 2, 0), ddy = N.B(lb, k, 2, 1) - N.A(i, 3, 2, 1),
-                 ddz = N.B(lb, k, 2, 2) - N.A(i, 3, 2, 2);
-          if (!(d2(ddx, ddy, ddz) < P.T_bond)) continue;
-          double ot = gettheta(N.A(i, 3, 1, 0) - N.A(i, 3, 2, 0), N.A(i, 3, 1, 1) - N.A(i, 3, 2, 1),
-                               N.A(i, 3, 1, 2) - N.A(i, 3, 2, 2), N.B(lb, k, 1, 0) - N.B(lb, k, 2, 0),
-                               N.B(lb, k, 1, 1) - N.B(lb, k, 2, 1), N.B(lb, k, 1, 2) - N.B(lb, k, 2, 2));
-          double pd = gettheta(N.A(i, 3, 1, 0) - N.A(i, 3, 4, 0), N.A(i, 3, 1, 1) - N.A(i, 3, 4, 1),
-                               N.A(i, 3, 1, 2) - N.A(i, 3, 4, 2), N.B(lb, 1, 1, 0) - N.B(lb, 1, 2, 0),
-                               N.B(lb, 1, 1, 1) - N.B(lb, 1, 2, 1), N.B(lb, 1, 1, 2) - N.B(lb, 1, 2, 2));
-          if (!((kmcm::fabs_(pd) < P.thetapd_cut) && (kmcm::fabs_(ot - 180) < P.thetaot_cut))) continue;
-          double u = kmcr::uniform(P.key, kmcr::DOM_RL, (uint32_t)i, (uint32_t)q, step, (uint32_t)k);
-          if (!(u < P.p_ass)) continue;
-          uint32_t pos = atomicAdd(&d.ctl->n_rl, 1u);
-          if (pos < d.cap_edges)
-            d.rl_keys[pos] = ((uint64_t)i << 34) | ((uint64_t)q << 2) | (uint64_t)(k - 2);
-          else
-            atomicOr(&d.ctl->err, ERR_EDGES);
-        }
       } else {
-        if (!want_cis || A_ST3(d, q) != 0) continue;
-        float dz = rp.z - fzl;
-        if (!(dxy2 < 57.0f * 57.0f) || !(dz * dz < 16.0f * 16.0f + 1.0f)) continue;
-        if (!record_final(d, id, step)) continue;
-        double ddx = N.A(q, 3, 3, 0) - N.A(i, 3, 3, 0), ddy = N.A(q, 3, 3, 1) - N.A(i, 3, 3, 1),
-               ddz = N.A(q, 3, 3, 2) - N.A(i, 3, 3, 2);
-        if (!(d2(ddx, ddy, ddz) < P.T_cis)) continue;
-        double ot = gettheta(N.A(i, 3, 1, 0) - N.A(i, 3, 3, 0), N.A(i, 3, 1, 1) - N.A(i, 3, 3, 1),
-                             N.A(i, 3, 1, 2) - N.A(i, 3, 3, 2), N.A(q, 3, 1, 0) - N.A(q, 3, 3, 0),
-                             N.A(q, 3, 1, 1) - N.A(q, 3, 3, 1), N.A(q, 3, 1, 2) - N.A(q, 3, 3, 2));
-        if (!(kmcm::fabs_(ot - 180) < P.cis_theta_cut)) continue;
-        double um = kmcr::uniform(P.key, kmcr::DOM_MONO, (uint32_t)i, (uint32_t)q, step, 0);
-        double uc = kmcr::uniform(P.key, kmcr::DOM_CIS, (uint32_t)i, (uint32_t)q, step, 0);
-        uint64_t fl = (um < P.p_mono ? 1u : 0u) | (uc < P.p_cis ? 2u : 0u);
-        if (!fl) continue;
-        uint32_t pos = atomicAdd(&d.ctl->n_cisc, 1u);
+        if (!want_cis || (id.x & RID_ST3)) continue;
+        if (!(dxy2 < 57.0f * 57.0f)) continue;
+        float gap = fmaxf(fmaxf(rp.z - fzh, fzl - rp.w), 0.0f);
+        if (!(gap < 16.0f)) continue;
+        if (!have_site) {
+          sx = (float)N.A(i, 3, 3, 0);
+          sy = (float)N.A(i, 3, 3, 1);
+          have_site = true;
+        }
+        float tx = (float)N.A(q, 3, 3, 0) - sx, ty = (float)N.A(q, 3, 3, 1) - sy;
+        if (!(tx * tx + ty * ty < 16.0f * 16.0f)) continue;
+      }
+      if (!record_final(d, id)) continue;
+      uint32_t pos = atomicAdd(&d.ctl->n_pairs, 1u);
+      if (pos < d.cap_pairs) d.pairs[pos] = make_int2(i, q);
+      else atomicOr(&d.ctl->err, ERR_EDGES);
+    }
+  }
+}
+
+// Reaction candidates, pass 2: exact R–L association gates (main.cpp:1880-1921)
+// and cis gates (1954-1985 / 2009-2039) on each pair; a pair becomes an
+// accepting edge when its keyed draw is below the acceptance probability.
+// The greedy kernels below replay the reference's loop order on the edges.
+__global__ void k_rxn_exact(KParams P, Dev d) {
+  const int NA = P.NA, NB = P.NB;
+  const uint32_t step = d.ctl->step;
+  const Beads& N = d.nxt;
+  uint32_t n = d.ctl->n_pairs;
+  if (n > d.cap_pairs) n = d.cap_pairs;
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+    int2 pr = d.pairs[t];
+    int i = pr.x, q = pr.y;
+    if (q >= NA) {
+      int lb = q - NA;
+      for (int k = 2; k <= 4; ++k) {
+        if (B_ST(d, lb, k) != 0) continue;
+        double ddx = N.B(lb, k, 2, 0) - N.A(i, 3, 2, 0), ddy = N.B(lb, k, 2, 1) - N.A(i, 3, 2, 1),
+               ddz = N.B(lb, k, 2, 2) - N.A(i, 3, 2, 2);
+        if (!(d2(ddx, ddy, ddz) < P.T_bond)) continue;
+        double ot = gettheta(N.A(i, 3, 1, 0) - N.A(i, 3, 2, 0), N.A(i, 3, 1, 1) - N.A(i, 3, 2, 1),
+                             N.A(i, 3, 1, 2) - N.A(i, 3, 2, 2), N.B(lb, k, 1, 0) - N.B(lb, k, 2, 0),
+                             N.B(lb, k, 1, 1) - N.B(lb, k, 2, 1), N.B(lb, k, 1, 2) - N.B(lb, k, 2, 2));
+        double pd = gettheta(N.A(i, 3, 1, 0) - N.A(i, 3, 4, 0), N.A(i, 3, 1, 1) - N.A(i, 3, 4, 1),
+                             N.A(i, 3, 1, 2) - N.A(i, 3, 4, 2), N.B(lb, 1, 1, 0) - N.B(lb, 1, 2, 0),
+                             N.B(lb, 1, 1, 1) - N.B(lb, 1, 2, 1), N.B(lb, 1, 1, 2) - N.B(lb, 1, 2, 2));
+        if (!((kmcm::fabs_(pd) < P.thetapd_cut) && (kmcm::fabs_(ot - 180) < P.thetaot_cut))) continue;
+        double u = kmcr::uniform(P.key, kmcr::DOM_RL, (uint32_t)i, (uint32_t)q, step, (uint32_t)k);
+        if (!(u < P.p_ass)) continue;
+        uint32_t pos = atomicAdd(&d.ctl->n_rl, 1u);
         if (pos < d.cap_edges)
-          d.cis_keys[pos] = ((uint64_t)i << 34) | ((uint64_t)q << 2) | fl;
+          d.rl_keys[pos] = ((uint64_t)i << 34) | ((uint64_t)q << 2) | (uint64_t)(k - 2);
         else
           atomicOr(&d.ctl->err, ERR_EDGES);
       }
+    } else {
+      double ddx = N.A(q, 3, 3, 0) - N.A(i, 3, 3, 0), ddy = N.A(q, 3, 3, 1) - N.A(i, 3, 3, 1),
+             ddz = N.A(q, 3, 3, 2) - N.A(i, 3, 3, 2);
+      if (!(d2(ddx, ddy, ddz) < P.T_cis)) continue;
+      double ot = gettheta(N.A(i, 3, 1, 0) - N.A(i, 3, 3, 0), N.A(i, 3, 1, 1) - N.A(i, 3, 3, 1),
+                           N.A(i, 3, 1, 2) - N.A(i, 3, 3, 2), N.A(q, 3, 1, 0) - N.A(q, 3, 3, 0),
+                           N.A(q, 3, 1, 1) - N.A(q, 3, 3, 1), N.A(q, 3, 1, 2) - N.A(q, 3, 3, 2));
+      if (!(kmcm::fabs_(ot - 180) < P.cis_theta_cut)) continue;
+      double um = kmcr::uniform(P.key, kmcr::DOM_MONO, (uint32_t)i, (uint32_t)q, step, 0);
+      double uc = kmcr::uniform(P.key, kmcr::DOM_CIS, (uint32_t)i, (uint32_t)q, step, 0);
+      uint64_t fl = (um < P.p_mono ? 1u : 0u) | (uc < P.p_cis ? 2u : 0u);
+      if (!fl) continue;
+      uint32_t pos = atomicAdd(&d.ctl->n_cisc, 1u);
+      if (pos < d.cap_edges)
+        d.cis_keys[pos] = ((uint64_t)i << 34) | ((uint64_t)q << 2) | fl;
+      else
+        atomicOr(&d.ctl->err, ERR_EDGES);
     }
   }
 }
@@ -1453,43 +1534,46 @@ __device__ __forceinline__ int wave_max(int v) {
   return v;
 }
 
-__global__ void k_observe(KParams P, Dev d) {
+__global__ void __launch_bounds__(256) k_observe(KParams P, Dev d) {
   const int NA = P.NA;
+  __shared__ int red[4][6];
   int p = blockIdx.x * blockDim.x + threadIdx.x;
-  int rl = 0, mono = 0, cis = 0, tp = 0, tc = 0, mx = 0;
+  int v[6] = {0, 0, 0, 0, 0, 0};  // rl mono cis tot_prot tot_clu max
   if (p < NA) {
-    rl = A_ST2(d, p);
+    v[0] = A_ST2(d, p);
     if (A_ST3(d, p) == 1) {
       int q = A_NEI3(d, p) - 1;
       if (p < q) {
-        if (A_ST2(d, p) == 0 && A_ST2(d, q) == 0) mono = 1;
-        else cis = 1;
+        if (A_ST2(d, p) == 0 && A_ST2(d, q) == 0) v[1] = 1;
+        else v[2] = 1;
       }
     }
   } else if (p < P.N) {
     uint8_t k = d.ukind[p];
     if (k == U_COMPLEX) {
       int s = d.cx_size[p - NA];
-      tp = s;
-      tc = 1;
-      mx = s;
+      v[3] = s;
+      v[4] = 1;
+      v[5] = s;
     } else if (k == U_FREE_B) {
-      mx = 1;
+      v[5] = 1;
     }
   }
-  rl = wave_sum(rl);
-  mono = wave_sum(mono);
-  cis = wave_sum(cis);
-  tp = wave_sum(tp);
-  tc = wave_sum(tc);
-  mx = wave_max(mx);
-  if ((threadIdx.x & 63) == 0) {
-    if (rl) atomicAdd(&d.ctl->rl, rl);
-    if (mono) atomicAdd(&d.ctl->mono, mono);
-    if (cis) atomicAdd(&d.ctl->cis, cis);
-    if (tp) atomicAdd(&d.ctl->tot_prot, tp);
-    if (tc) atomicAdd(&d.ctl->tot_clu, tc);
-    if (mx) atomicMax(&d.ctl->max_size, mx);
+  for (int f = 0; f < 5; ++f) v[f] = wave_sum(v[f]);
+  v[5] = wave_max(v[5]);
+  int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0)
+    for (int f = 0; f < 6; ++f) red[w][f] = v[f];
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    int f = threadIdx.x, a = red[0][f];
+    for (int ww = 1; ww < 4; ++ww) a = f == 5 ? max(a, red[ww][f]) : a + red[ww][f];
+    if (a) {
+      int* dst = f == 0 ? &d.ctl->rl : f == 1 ? &d.ctl->mono : f == 2 ? &d.ctl->cis : f == 3 ? &d.ctl->tot_prot
+                 : f == 4 ? &d.ctl->tot_clu : &d.ctl->max_size;
+      if (f == 5) atomicMax(dst, a);
+      else atomicAdd(dst, a);
+    }
   }
 }
 
@@ -1512,6 +1596,17 @@ __global__ void k_finalize(KParams P, Dev d, double time_step) {
   d.obs[c->obs_idx] = o;
   c->obs_idx = c->obs_idx + 1;
   c->step = c->step + 1;
+  // per-step counters for the next step (the former k_begin)
+  c->n_units = 0;
+  c->n_overflow = 0;
+  c->cx_cursor = 0;
+  c->n_wl[0] = 0;
+  c->n_wl[1] = 0;
+  c->n_rl = 0;
+  c->n_cisc = 0;
+  c->n_pairs = 0;
+  c->rl = c->mono = c->cis = 0;
+  c->tot_prot = c->tot_clu = c->max_size = 0;
 }
 
 }  // namespace kmcd
