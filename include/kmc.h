@@ -142,6 +142,12 @@ int kmc_set_timing(kmc_sim* s, uint64_t kernel_mask);
 int kmc_kernel_times(const kmc_sim* s, double* total_ms, int64_t* launches, int32_t n);
 const char* kmc_kernel_name(int32_t id);
 
+/* BFS member rows of the last simulated step (results[i][.] of main.cpp:537,
+ * after the multi-ligand shuffles): for each ligand b, row_len[b] members
+ * (reference 1-based indices) are appended to `members` (n_a+n_b capacity);
+ * non-root ligands have row_len 0.  Feeds cluster.log (main.cpp:2291-2305). */
+int kmc_get_clusters(kmc_sim* s, int32_t* row_len, int32_t* members);
+
 /* Formatting helpers shared by every host driver.  Each returns the number of
  * characters written (excluding NUL) or < 0. */
 int kmc_format_bond_line(const kmc_params* p, const kmc_obs* o, char* buf, size_t n);   /* main.cpp:2251 */
@@ -157,6 +163,12 @@ const char* kmc_host_last_error(void);
 int kmc_host_load_cpt(const kmc_params* p, const char* path, kmc_state_view* v);
 int kmc_host_write_cpt(const kmc_params* p, const kmc_state_view* v, const char* path);
 int kmc_host_init_random(const kmc_params* p, kmc_state_view* v);
+/* parameter.log (main.cpp:178-205), test.gro frame (2258-2287, appended),
+ * cluster.log block (2291-2305, appended) */
+int kmc_host_write_parameter_log(const kmc_params* p, const char* path);
+int kmc_host_append_gro(const kmc_params* p, const kmc_state_view* v, const char* path);
+int kmc_host_append_cluster_log(const kmc_params* p, int64_t step, const int32_t* row_len, const int32_t* members,
+                                const char* path);
 /* bond-link consistency + rigid-body extent bound; KMC_OK or an error code */
 int kmc_host_validate(const kmc_params* p, const kmc_state_view* v);
 

@@ -15,6 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libkmc.so")
+RUN = os.path.join(LIB_DIR, "kmc_run")
 SOURCES = ["kmc_engine.hip", "kmc_io.cpp"]
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
@@ -39,7 +40,7 @@ def _inputs():
 
 
 def stale() -> bool:
-    if not os.path.exists(LIB):
+    if not os.path.exists(LIB) or not os.path.exists(RUN):
         return True
     t = os.path.getmtime(LIB)
     return any(os.path.getmtime(f) > t for f in _inputs())
@@ -48,6 +49,24 @@ def stale() -> bool:
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not stale():
         return LIB
+    _build_lib(verbose)
+    _build_driver(verbose)
+    return LIB
+
+
+def _build_driver(verbose: bool) -> None:
+    """kmc_run: the drop-in executable (host C++, links libkmc.so)."""
+    cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-o", RUN, os.path.join(CSRC, "kmc_run.cpp"),
+           "-L" + LIB_DIR, "-lkmc", "-Wl,-rpath,$ORIGIN"]
+    if verbose:
+        print(" ".join(cmd))
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError("g++ failed building kmc_run")
+
+
+def _build_lib(verbose: bool) -> str:
     os.makedirs(LIB_DIR, exist_ok=True)
     tmp = LIB + ".tmp"
     cmd = [HIPCC, *FLAGS, "-o", tmp, *[os.path.join(CSRC, s) for s in SOURCES]]

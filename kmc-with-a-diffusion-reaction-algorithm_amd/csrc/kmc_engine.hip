@@ -388,12 +388,13 @@ static int launch_step(kmc_sim* s) {
   });
   TIMED(KI_REC_SCATTER, (k_rec_scatter<<<gN, T, 0, st>>>(K, d)));
   const int gR = (2 * K.N + T - 1) / T;
-  TIMED(KI_RESOLVE0, (k_resolve0<<<gR, T, 0, st>>>(K, d)));
+  const int ntiles = ((K.ncx + TILE - 1) / TILE) * ((K.ncy + TILE - 1) / TILE);
+  TIMED(KI_RESOLVE0, (k_resolve0_tile<<<ntiles, 256, 0, st>>>(K, d)));
   TIMED(KI_RESOLVE1, (k_resolve<<<gN, T, 0, st>>>(K, d, 0)));
   TIMED(KI_RESOLVE_TAIL, (k_resolve_tail<<<1, 1024, 0, st>>>(K, d)));
   TIMED(KI_COMMIT, (k_commit<<<gN, T, 0, st>>>(K, d)));
   if (K.NA > 0) {
-    TIMED(KI_RXN_SCAN, (k_rxn_scan<<<gR, T, 0, st>>>(K, d)));
+    TIMED(KI_RXN_SCAN, (k_rxn_scan_tile<<<ntiles, 256, 0, st>>>(K, d)));
     TIMED(KI_RXN_EXACT, (k_rxn_exact<<<1024, T, 0, st>>>(K, d)));
     TIMED(KI_RL_MATCH, (k_rl_match<<<1, 1024, 0, st>>>(K, d)));
     TIMED(KI_CIS_MATCH, (k_cis_match<<<1, 1024, 0, st>>>(K, d)));
@@ -481,6 +482,33 @@ int kmc_device_math(int op, const double* x, const double* y, double* out, int64
   (void)hipFree(dy);
   (void)hipFree(dout);
   return rc;
+}
+
+int kmc_get_clusters(kmc_sim* s, int32_t* row_len, int32_t* members) {
+  if (!s || !row_len || !members) return KMC_ERR_ARG;
+  if (s->step_done == 0 || !s->have_state) return fail(s, KMC_ERR_ARG, "no step simulated yet");
+  const int NA = s->p.n_a, NB = s->p.n_b, N = NA + NB;
+  std::vector<uint8_t> kind(N);
+  std::vector<int32_t> off(NB), size(NB), mem(N);
+  HIPCHK(s, hipStreamSynchronize(s->stream));
+  HIPCHK(s, hipMemcpy(kind.data(), s->d.ukind, N, hipMemcpyDeviceToHost));
+  HIPCHK(s, hipMemcpy(off.data(), s->d.cx_off, sizeof(int32_t) * NB, hipMemcpyDeviceToHost));
+  HIPCHK(s, hipMemcpy(size.data(), s->d.cx_size, sizeof(int32_t) * NB, hipMemcpyDeviceToHost));
+  HIPCHK(s, hipMemcpy(mem.data(), s->d.members, sizeof(int32_t) * N, hipMemcpyDeviceToHost));
+  int64_t o = 0;
+  for (int b = 0; b < NB; ++b) {
+    int p = NA + b;
+    if (kind[p] == U_FREE_B) {
+      row_len[b] = 1;
+      members[o++] = p + 1;
+    } else if (kind[p] == U_COMPLEX) {
+      row_len[b] = size[b];
+      for (int t = 0; t < size[b]; ++t) members[o++] = mem[off[b] + t] + 1;
+    } else {
+      row_len[b] = 0;
+    }
+  }
+  return KMC_OK;
 }
 
 int kmc_set_timing(kmc_sim* s, uint64_t kernel_mask) {

@@ -456,6 +456,70 @@ int kmc_format_bond_line(const kmc_params* p, const kmc_obs* o, char* buf, size_
 
 uint64_t kmc_state_hash(const kmc_params* p, const kmc_state_view* v) { return kmch::state_hash(p->n_a, p->n_b, v); }
 
+// parameter.log, main.cpp:178-205 (default ostream float format = %g)
+int kmc_host_write_parameter_log(const kmc_params* p, const char* path) {
+  FILE* f = fopen(path, "wb");
+  if (!f) return KMC_ERR_IO;
+  auto L = [&](const char* k, double v) { fprintf(f, "%25s%15g\n", k, v); };
+  fprintf(f, "%25s%15g%7g%7g\n\n", "box size: x y z", p->box_x, p->box_y, p->box_z);
+  fprintf(f, "%25s%15d\n", "protein_A_tot_num", p->n_a);
+  fprintf(f, "%25s%15d\n", "RB_A_tot_num", p->n_a * 4);
+  fprintf(f, "%25s%15d\n", "protein_B_tot_num", p->n_b);
+  fprintf(f, "%25s%15d\n\n", "RB_B_tot_num", p->n_b * 4);
+  L("RB_A_D", p->ra_D);
+  L("RB_A_rot_D", p->ra_rot_D);
+  L("RB_B_D", p->rb_D);
+  fprintf(f, "%25s%15g\n\n", "RB_B_rot_D", p->rb_rot_D);
+  fprintf(f, "%25s\n", "R-L interaction:");
+  L("bond_D", p->bond_D);
+  L("bond_rot_D", p->bond_rot_D);
+  L("Ass_Rate", p->ass_rate);
+  fprintf(f, "%25s%15g\n\n", "Diss_Rate", p->diss_rate);
+  fprintf(f, "%25s\n", "Cis interaction:");
+  L("cis_D", p->cis_D);
+  L("cis_rot_D", p->cis_rot_D);
+  L("mono_cis_Ass_Rate", p->mono_cis_ass_rate);
+  fprintf(f, "%25s%15g\n\n", "mono_cis_Diss_Rate", p->mono_cis_diss_rate);
+  L("cis_Ass_Rate", p->cis_ass_rate);
+  fprintf(f, "%25s%15g\n\n", "cis_Diss_Rate", p->cis_diss_rate);
+  return fclose(f) == 0 ? KMC_OK : KMC_ERR_IO;
+}
+
+// test.gro frame, main.cpp:2258-2287 (appended): receptor domain centres and
+// ligand subunit centres in nm, fixed with 3 decimals
+int kmc_host_append_gro(const kmc_params* p, const kmc_state_view* v, const char* path) {
+  FILE* f = fopen(path, "ab");
+  if (!f) return KMC_ERR_IO;
+  const int na = p->n_a, nb = p->n_b;
+  fprintf(f, "Hello Gro!, t=%.3f\n", (double)(int)v->step * p->time_step);
+  fprintf(f, "%d\n", na * 4 + nb * 3);
+  for (int i = 0; i < na; ++i)
+    for (int j = 1; j <= 4; ++j)
+      fprintf(f, "%5dALA%7s%5d%8.3f%8.3f%8.3f\n", i + 1, "CA", i + 1, v->ra[RA(na, j, 1, 0, i)] / 10,
+              v->ra[RA(na, j, 1, 1, i)] / 10, v->ra[RA(na, j, 1, 2, i)] / 10);
+  for (int b = 0; b < nb; ++b)
+    for (int j = 2; j <= 4; ++j)
+      fprintf(f, "%5dLEU%7s%5d%8.3f%8.3f%8.3f\n", na + b + 1, "CA", na + b + 1, v->rb[RB(nb, j, 1, 0, b)] / 10,
+              v->rb[RB(nb, j, 1, 1, b)] / 10, v->rb[RB(nb, j, 1, 2, b)] / 10);
+  fprintf(f, "%8.3f%12.3f%12.3f\n", p->box_x / 10, p->box_y / 10, p->box_z / 10);
+  return fclose(f) == 0 ? KMC_OK : KMC_ERR_IO;
+}
+
+// cluster.log block, main.cpp:2291-2305 (appended): for every ligand its BFS
+// row (members in results[i][.] order, "  "-separated; empty for non-roots)
+int kmc_host_append_cluster_log(const kmc_params* p, int64_t step, const int32_t* row_len, const int32_t* members,
+                                const char* path) {
+  FILE* f = fopen(path, "ab");
+  if (!f) return KMC_ERR_IO;
+  fprintf(f, "Hello Cluster!, t=%g\n", (double)(int)step * p->time_step);
+  int64_t o = 0;
+  for (int b = 0; b < p->n_b; ++b) {
+    for (int t = 0; t < row_len[b]; ++t) fprintf(f, "%d  ", members[o++]);
+    fputc('\n', f);
+  }
+  return fclose(f) == 0 ? KMC_OK : KMC_ERR_IO;
+}
+
 static thread_local std::string g_host_err;
 const char* kmc_host_last_error(void) { return g_host_err.c_str(); }
 

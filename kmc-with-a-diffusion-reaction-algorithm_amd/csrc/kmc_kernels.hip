@@ -1110,6 +1110,200 @@ __global__ void k_resolve0(KParams P, Dev d) {
   }
 }
 
+// ---------------------------------------------------------------- LDS tiles
+// A workgroup owns a TILE×TILE block of cells.  It stages the records of the
+// block plus a one-cell halo into LDS with coalesced row loads (a halo row of
+// cells is one contiguous record range of the cell-sorted array), then every
+// thread scans its records' 3x3 neighbourhoods from LDS.  Only prefilter hits
+// touch global memory (unit state, exact fp64 beads).
+#define TILE 16
+#define HALO (TILE + 2)
+#define TCAP 1280
+struct TileLds {
+  float4 pos[TCAP];
+  int2 id[TCAP];
+  int cstart[HALO][HALO + 1];  // LDS index of each halo cell's first record (+ row end)
+  int g0[HALO];                // global index of each halo row's first record
+  int n;
+  int overflow;
+};
+
+// returns false if the tile does not fit TCAP (caller falls back to global)
+__device__ bool tile_load(const KParams& P, const Dev& d, int tx, int ty, TileLds& T) {
+  const int cx0 = tx * TILE - 1, cy0 = ty * TILE - 1;
+  const int xlo = max(cx0, 0), xhi = min(cx0 + HALO - 1, P.ncx - 1);
+  // 1. raw cell boundaries (global record indices), one per thread
+  for (int idx = threadIdx.x; idx < HALO * (HALO + 1); idx += blockDim.x) {
+    int hy = idx / (HALO + 1), hx = idx % (HALO + 1);
+    int y = cy0 + hy;
+    int v = 0;
+    if (y >= 0 && y < P.ncy && xlo <= xhi) {
+      int x = min(max(cx0 + hx, xlo), xhi + 1);
+      v = d.cell_start[y * P.ncx + x];
+    }
+    T.cstart[hy][hx] = v;
+  }
+  __syncthreads();
+  // 2. row bases in LDS
+  if (threadIdx.x == 0) {
+    int n = 0;
+    for (int hy = 0; hy < HALO; ++hy) {
+      T.g0[hy] = T.cstart[hy][0];
+      int len = T.cstart[hy][HALO] - T.cstart[hy][0];
+      T.cstart[hy][HALO] = n;  // temporarily: LDS row base
+      n += len;
+    }
+    T.n = n;
+    T.overflow = n > TCAP;
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < HALO * (HALO + 1); idx += blockDim.x) {
+    int hy = idx / (HALO + 1), hx = idx % (HALO + 1);
+    if (hx == HALO) continue;
+    T.cstart[hy][hx] = T.cstart[hy][HALO] + (T.cstart[hy][hx] - T.g0[hy]);
+  }
+  __syncthreads();
+  if (threadIdx.x < HALO) {  // row end = next row's base
+    int hy = threadIdx.x;
+    T.cstart[hy][HALO] = hy + 1 < HALO ? T.cstart[hy + 1][0] : T.n;
+  }
+  __syncthreads();
+  if (T.overflow) return false;
+  // 3. copy every halo row's contiguous record range
+  for (int hy = 0; hy < HALO; ++hy) {
+    int lo = T.cstart[hy][0], hi = T.cstart[hy][HALO];
+    int g0 = T.g0[hy];
+    for (int t = threadIdx.x; t < hi - lo; t += blockDim.x) {
+      T.pos[lo + t] = d.rec_pos[g0 + t];
+      T.id[lo + t] = d.rec_id[g0 + t];
+    }
+  }
+  __syncthreads();
+  return true;
+}
+
+// interior records of the tile (halo rows 1..TILE, cells 1..TILE) as one flat
+// index space: thread t takes the t-th interior record of the tile
+__device__ __forceinline__ int interior_count(const TileLds& T) {
+  int n = 0;
+  for (int hy = 1; hy <= TILE; ++hy) n += T.cstart[hy][TILE + 1] - T.cstart[hy][1];
+  return n;
+}
+__device__ __forceinline__ int interior_record(const TileLds& T, int t, int* hy_out, int* hx_out) {
+  int hy = 1;
+  for (;; ++hy) {
+    int len = T.cstart[hy][TILE + 1] - T.cstart[hy][1];
+    if (t < len) break;
+    t -= len;
+  }
+  int r = T.cstart[hy][1] + t;
+  int hx = 1;
+  while (T.cstart[hy][hx + 1] <= r) ++hx;
+  *hy_out = hy;
+  *hx_out = hx;
+  return r;
+}
+
+// single-member unit u (free receptor / free ligand) whose proposal record is
+// at halo cell (hx, hy) of the tile
+__device__ uint32_t evaluate_single_lds(const KParams& P, const Dev& d, const TileLds& T, int u, float4 me, int hx,
+                                        int hy, uint32_t step) {
+  const int NA = P.NA;
+  const bool mA = u < NA;
+  bool blocked = false, loaded = false;
+  Own o;
+  for (int yy = hy - 1; yy <= hy + 1; ++yy) {
+    int r0 = T.cstart[yy][hx - 1], r1 = T.cstart[yy][hx + 2];
+    for (int r = r0; r < r1; ++r) {
+      int2 id = T.id[r];
+      int q = id.x & RID_PID;
+      if (q == u) continue;
+      if (!prefilter(mA, me.x, me.y, me.z, me.w, q < NA, T.pos[r])) continue;
+      bool isnew = id.x < 0;
+      int kq = id.y;
+      bool pending = false;
+      if (kq < 0) {
+        atomicOr(&d.ctl->err, ERR_RESOLVE);
+        continue;
+      }
+      if (kq > u) {
+        if (isnew) continue;
+      } else {  // kq < u (a single-member unit owns only itself)
+        uint32_t st = state_of(d, kq, step);
+        if (st == S_ACC) {
+          if (!isnew) continue;
+        } else if (st == S_REJ) {
+          if (isnew) continue;
+        } else {
+          pending = true;
+        }
+      }
+      if (!loaded) {
+        load_own(P, d.nxt, u, o);
+        loaded = true;
+      }
+      if (exact_collide(P, o, isnew ? d.nxt : d.cur, q)) {
+        if (!pending) return S_REJ;
+        blocked = true;
+      }
+    }
+  }
+  return blocked ? S_UND : S_ACC;
+}
+
+__device__ __forceinline__ void resolve_emit(const Dev& d, int u, uint32_t step, uint32_t s) {
+  if (s == S_UND) {
+    uint32_t pos = atomicAdd(&d.ctl->n_wl[0], 1u);
+    d.wl0[pos] = u;
+  } else {
+    set_state(d, u, step, s);
+  }
+}
+
+// round 0, tiled: every unit keyed at a proposal record inside the tile
+__global__ void __launch_bounds__(256) k_resolve0_tile(KParams P, Dev d) {
+  __shared__ TileLds T;
+  const int ntx = (P.ncx + TILE - 1) / TILE;
+  const int tx = blockIdx.x % ntx, ty = blockIdx.x / ntx;
+  const uint32_t step = d.ctl->step;
+  const int cx0 = tx * TILE - 1, cy0 = ty * TILE - 1;
+  if (!tile_load(P, d, tx, ty, T)) {
+    // dense tile: scan the block's interior records from global memory
+    for (int hy = 1; hy <= TILE; ++hy) {
+      int y = cy0 + hy;
+      if (y < 0 || y >= P.ncy) continue;
+      int xlo = max(cx0 + 1, 0), xhi = min(cx0 + TILE, P.ncx - 1);
+      if (xlo > xhi) continue;
+      int r0 = d.cell_start[y * P.ncx + xlo], r1 = d.cell_start[y * P.ncx + xhi + 1];
+      for (int r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
+        int2 id = d.rec_id[r];
+        if (id.x >= 0) continue;
+        int u = id.x & RID_PID;
+        if (id.y != u || d.ukind[u] == U_NONE) continue;
+        float4 ref = d.rec_pos[r];
+        resolve_emit(d, u, step, evaluate_unit(P, d, u, step, &ref));
+      }
+    }
+    return;
+  }
+  const int nint = interior_count(T);
+  for (int t = threadIdx.x; t < nint; t += blockDim.x) {
+    int hy, hx;
+    int r = interior_record(T, t, &hy, &hx);
+    int2 id = T.id[r];
+    if (id.x >= 0) continue;  // old-position record
+    int u = id.x & RID_PID;
+    if (id.y != u) continue;
+    uint8_t kind = d.ukind[u];
+    if (kind == U_NONE) continue;
+    float4 me = T.pos[r];
+    uint32_t s;
+    if (kind == U_FREE_A || kind == U_FREE_B) s = evaluate_single_lds(P, d, T, u, me, hx, hy, step);
+    else s = evaluate_unit(P, d, u, step, &me);  // dimer / complex: members anywhere
+    resolve_emit(d, u, step, s);
+  }
+}
+
 // round 1: the units round 0 left undecided
 __global__ void k_resolve(KParams P, Dev d, int src) {
   const uint32_t step = d.ctl->step;
@@ -1245,6 +1439,112 @@ __global__ void k_rxn_scan(KParams P, Dev d) {
       uint32_t pos = atomicAdd(&d.ctl->n_pairs, 1u);
       if (pos < d.cap_pairs) d.pairs[pos] = make_int2(i, q);
       else atomicOr(&d.ctl->err, ERR_EDGES);
+    }
+  }
+}
+
+// reaction scan, tiled: final records of receptors inside the tile
+__device__ void rxn_scan_one(const KParams& P, const Dev& d, const TileLds* T, int i, int2 me, float4 mp, int hx,
+                             int hy, int gcx, int gcy) {
+  const int NA = P.NA, NB = P.NB;
+  const Beads& N = d.nxt;
+  bool want_rl = !(me.x & RID_ST2) && NB > 0;
+  bool want_cis = !(me.x & RID_ST3);
+  float fx = mp.x, fy = mp.y, fzl = mp.z, fzh = mp.w;
+  float sx = 0, sy = 0;
+  bool have_site = false;
+  for (int dy = -1; dy <= 1; ++dy) {
+    int r0, r1;
+    if (T) {
+      r0 = T->cstart[hy + dy][hx - 1];
+      r1 = T->cstart[hy + dy][hx + 2];
+    } else {
+      int yy = gcy + dy;
+      if (yy < 0 || yy >= P.ncy) continue;
+      int x0 = gcx > 0 ? gcx - 1 : 0, x1 = gcx + 1 < P.ncx ? gcx + 1 : P.ncx - 1;
+      r0 = d.cell_start[yy * P.ncx + x0];
+      r1 = d.cell_start[yy * P.ncx + x1 + 1];
+    }
+    for (int rr = r0; rr < r1; ++rr) {
+      int2 id = T ? T->id[rr] : d.rec_id[rr];
+      int q = id.x & RID_PID;
+      if (q == i) continue;
+      float4 rp = T ? T->pos[rr] : d.rec_pos[rr];
+      float dx = rp.x - fx, dy2 = rp.y - fy;
+      float dxy2 = dx * dx + dy2 * dy2;
+      if (q >= NA) {
+        if (!want_rl) continue;
+        if (!(dxy2 < 105.0f * 105.0f) || !(rp.z > fzl - 85.0f && rp.z < fzh + 85.0f)) continue;
+      } else {
+        if (!want_cis || (id.x & RID_ST3)) continue;
+        if (!(dxy2 < 57.0f * 57.0f)) continue;
+        float gap = fmaxf(fmaxf(rp.z - fzh, fzl - rp.w), 0.0f);
+        if (!(gap < 16.0f)) continue;
+        if (!have_site) {
+          sx = (float)N.A(i, 3, 3, 0);
+          sy = (float)N.A(i, 3, 3, 1);
+          have_site = true;
+        }
+        float tx = (float)N.A(q, 3, 3, 0) - sx, ty = (float)N.A(q, 3, 3, 1) - sy;
+        if (!(tx * tx + ty * ty < 16.0f * 16.0f)) continue;
+      }
+      if (!record_final(d, id)) continue;
+      uint32_t pos = atomicAdd(&d.ctl->n_pairs, 1u);
+      if (pos < d.cap_pairs) d.pairs[pos] = make_int2(i, q);
+      else atomicOr(&d.ctl->err, ERR_EDGES);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) k_rxn_scan_tile(KParams P, Dev d) {
+  __shared__ TileLds T;
+  const int ntx = (P.ncx + TILE - 1) / TILE;
+  const int tx = blockIdx.x % ntx, ty = blockIdx.x / ntx;
+  const int cx0 = tx * TILE - 1, cy0 = ty * TILE - 1;
+  const int NA = P.NA;
+  bool lds = tile_load(P, d, tx, ty, T);
+  if (lds) {
+    const int nint = interior_count(T);
+    for (int t = threadIdx.x; t < nint; t += blockDim.x) {
+      int hy, hx;
+      int r = interior_record(T, t, &hy, &hx);
+      int2 me = T.id[r];
+      int i = me.x & RID_PID;
+      if (i >= NA) continue;
+      if ((me.x & RID_ST2) && (me.x & RID_ST3)) continue;
+      if (!record_final(d, me)) continue;
+      rxn_scan_one(P, d, &T, i, me, T.pos[r], hx, hy, 0, 0);
+    }
+    return;
+  }
+  for (int hy = 1; hy <= TILE; ++hy) {
+    int y = cy0 + hy;
+    if (y < 0 || y >= P.ncy) continue;
+    int r0, r1;
+    if (lds) {
+      r0 = T.cstart[hy][1];
+      r1 = T.cstart[hy][TILE + 1];
+    } else {
+      int xlo = max(cx0 + 1, 0), xhi = min(cx0 + TILE, P.ncx - 1);
+      if (xlo > xhi) continue;
+      r0 = d.cell_start[y * P.ncx + xlo];
+      r1 = d.cell_start[y * P.ncx + xhi + 1];
+    }
+    for (int r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
+      int2 me = lds ? T.id[r] : d.rec_id[r];
+      int i = me.x & RID_PID;
+      if (i >= NA) continue;
+      if ((me.x & RID_ST2) && (me.x & RID_ST3)) continue;
+      if (!record_final(d, me)) continue;
+      float4 mp = lds ? T.pos[r] : d.rec_pos[r];
+      if (lds) {
+        int hx = 1;
+        while (T.cstart[hy][hx + 1] <= r) ++hx;
+        rxn_scan_one(P, d, &T, i, me, mp, hx, hy, 0, 0);
+      } else {
+        double ax = d.nxt.A(i, 1, 1, 0), ay = d.nxt.A(i, 1, 1, 1);
+        rxn_scan_one(P, d, nullptr, i, me, mp, 0, 0, cell_x(P, ax), cell_y(P, ay));
+      }
     }
   }
 }

@@ -66,6 +66,10 @@ def load_library(path: Optional[str] = None):
     L.kmc_host_write_cpt.argtypes = [P(capi.Params), P(capi.StateView), C.c_char_p]
     L.kmc_host_init_random.argtypes = [P(capi.Params), P(capi.StateView)]
     L.kmc_host_validate.argtypes = [P(capi.Params), P(capi.StateView)]
+    L.kmc_get_clusters.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    L.kmc_host_write_parameter_log.argtypes = [P(capi.Params), C.c_char_p]
+    L.kmc_host_append_gro.argtypes = [P(capi.Params), P(capi.StateView), C.c_char_p]
+    L.kmc_host_append_cluster_log.argtypes = [P(capi.Params), C.c_int64, C.c_void_p, C.c_void_p, C.c_char_p]
     for f in ("kmc_host_math", "kmc_device_math"):
         getattr(L, f).argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]
     _lib = L
@@ -120,6 +124,25 @@ def bond_line(params: capi.Params, rec) -> str:
     buf = C.create_string_buffer(256)
     n = load_library().kmc_format_bond_line(C.byref(params), C.byref(o), buf, 256)
     return buf.value[:n].decode()
+
+
+def write_parameter_log(params: capi.Params, path: str) -> None:
+    """parameter.log (main.cpp:178-205)."""
+    _host_check(load_library().kmc_host_write_parameter_log(C.byref(params), os.fsencode(path)))
+
+
+def append_gro(params: capi.Params, hs: capi.HostState, path: str) -> None:
+    """one test.gro frame (main.cpp:2258-2287)."""
+    v = hs.view()
+    _host_check(load_library().kmc_host_append_gro(C.byref(params), C.byref(v), os.fsencode(path)))
+
+
+def append_cluster_log(params: capi.Params, step: int, row_len: np.ndarray, members: np.ndarray, path: str) -> None:
+    """one cluster.log block (main.cpp:2291-2305)."""
+    row_len = np.ascontiguousarray(row_len, dtype=np.int32)
+    members = np.ascontiguousarray(members, dtype=np.int32)
+    _host_check(load_library().kmc_host_append_cluster_log(C.byref(params), step, row_len.ctypes.data,
+                                                           members.ctypes.data, os.fsencode(path)))
 
 
 def math(op: int, x: np.ndarray, y: Optional[np.ndarray] = None, device: bool = False) -> np.ndarray:
@@ -195,6 +218,13 @@ class Simulation:
             out = np.zeros(n, dtype=capi.OBS_DTYPE)
         self._check(load_library().kmc_step(self._h, n, out.ctypes.data_as(C.c_void_p)))
         return out
+
+    def clusters(self):
+        """BFS member rows of the last step: (row_len[n_b], members) — kmc_get_clusters."""
+        row = np.zeros(self.params.n_b, dtype=np.int32)
+        mem = np.zeros(self.params.n_a + self.params.n_b, dtype=np.int32)
+        self._check(load_library().kmc_get_clusters(self._h, row.ctypes.data, mem.ctypes.data))
+        return row, mem[: int(row.sum())]
 
     @property
     def current_step(self) -> int:

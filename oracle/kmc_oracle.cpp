@@ -1284,6 +1284,17 @@ int oracle_step(oracle_t* h, int64_t n, kmc_obs* obs, uint64_t* hashes) {
 }
 
 uint64_t oracle_hash(oracle_t* h) { return h->o->hash(); }
+// results rows of the last step (main.cpp:537 + shuffles), kmc_get_clusters format
+int oracle_get_clusters(oracle_t* h, int32_t* row_len, int32_t* members) {
+  Oracle& o = *h->o;
+  int64_t k = 0;
+  for (int b = 0; b < o.NB; ++b) {
+    const std::vector<int>& r = o.results[o.NA + 1 + b];
+    row_len[b] = (int32_t)r.size();
+    for (int m : r) members[k++] = m;
+  }
+  return 0;
+}
 // event counters: free_a dimer free_b complex laydown multi repeat reject
 //                 rl mono cis rld md cd snap_bond snap_cis
 int oracle_stats(oracle_t* h, int64_t* out, int n) {

@@ -55,7 +55,7 @@ SCENARIOS = {
         t0=4242,
         steps=20000,
         params=DENSE,
-        dump=[8000, 15000, 20000],
+        dump=[4999, 8000, 9999, 15000, 20000],
         keep=[(0, 2000), (8000, 10000), (15000, 16000)],
         cpt_at=[5000, 10000, 15000, 20000],
     ),
@@ -136,8 +136,14 @@ def run_scenario(name, sc):
         with gzip.GzipFile(os.path.join(HERE, f"{name}_{s}.cpt.gz"), "wb", mtime=0) as f:
             f.write(data)
     bond = os.path.join(tmp, "bond.dat")
-    if os.path.exists(bond):
+    if os.path.exists(bond) and os.path.getsize(bond):
         shutil.copy(bond, os.path.join(HERE, f"{name}_bond.dat"))
+    # the reference's other outputs (main.cpp:178-205, 2258-2305)
+    for fn in ("parameter.log", "test.gro", "cluster.log"):
+        src = os.path.join(tmp, fn)
+        if os.path.exists(src) and os.path.getsize(src):
+            with open(src, "rb") as f, gzip.GzipFile(os.path.join(HERE, f"{name}_{fn}.gz"), "wb", mtime=0) as g:
+                g.write(f.read())
     shutil.rmtree(tmp)
     print(name, "rows", len(rows), "kept", int(mask.sum()), "cpts", sorted(seen))
 
