@@ -41,14 +41,14 @@ def kernel_bytes(name: str, n_a: int, n_b: int):
     models = {
         # read R (16 receptor / 8 ligand beads × xyz × 8 B), write R_new, unit kind
         "k_propose": 768 * n_a + 384 * n_b + n,
-        # own proposal's collision beads (12 doubles) + every record once
-        # (float4 + id) + owner/state of each record's unit
-        "k_resolve_r0": 96 * n + 2 * n * 20 + 2 * n * 8,
-        # old + new reference points (x, y, zlo, zhi), record write, cell cursor
-        "k_rec_scatter": 2 * n * 32 + 2 * n * 20 + 2 * n * 8,
+        # every record once (float4 + id); candidate writes are data-dependent
+        "k_col_scan": 2 * n * 24,
+        # old + new reference points (x, y, zlo, zhi) + receptor site, record
+        # write (pos, id, site), owner, cell cursor
+        "k_rec_scatter": 2 * n * 32 + 2 * n_a * 16 + 2 * n * 32 + 4 * n + 2 * n * 8,
         "k_rec_count": 2 * n * 32 + 2 * n * 4 + 48 * n_a + 48 * n_b,
-        # final records + receptor site beads
-        "k_rxn_candidates": 2 * n * 20 + 2 * n * 8 + 96 * n_a,
+        # every record once (float4 + id + site) + final flags
+        "k_rxn_scan": 2 * n * 32 + n,
         "k_commit": 8 * n,
         "k_classify": 20 * n_a + 12 * n_b + 5 * n,
         "k_observe": 16 * n_a + 5 * n_b,

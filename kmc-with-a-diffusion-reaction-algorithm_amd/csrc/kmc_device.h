@@ -28,6 +28,7 @@ struct KParams {
   // exact squared-distance thresholds: sqrt(s) < c  <=>  s < T(c)
   double T_aa, T_ab, T_bb, T_bond, T_cis;
   kmcr::Key key;
+  int tcap;  // LDS tile record capacity (<= TCAP; lowered only to test the global path)
 };
 
 // per-step control block in device memory (replayable without host writes)
@@ -37,10 +38,12 @@ struct Ctl {
   uint32_t err;           // error bits (ERR_*)
   uint32_t pad0;
   // per-step work-list counters
-  uint32_t n_units;       // units (keys) this step
   uint32_t n_overflow;    // ligands whose BFS overflowed the register queue
   uint32_t cx_cursor;     // members[] allocation cursor
-  uint32_t n_wl[2];       // resolution work lists
+  uint32_t n_cand;        // collision candidates (resolution pass A)
+  uint32_t n_conf;        // conflict entries (pass B)
+  uint32_t n_plist;       // units with conflict entries
+  uint32_t n_pend;        // units still pending after a round (pass C)
   uint32_t n_rl;          // R–L accepting edges
   uint32_t n_cisc;        // cis candidates
   uint32_t n_pairs;       // reaction (receptor, record) pairs
@@ -63,7 +66,7 @@ enum : uint32_t {
 };
 
 enum : uint8_t { U_NONE = 0, U_FREE_A = 1, U_DIMER = 2, U_FREE_B = 3, U_COMPLEX = 4 };
-enum : uint32_t { S_UND = 0, S_ACC = 1, S_REJ = 2 };
+enum : uint32_t { S_ACC = 1, S_PEND = 2, S_REJ = 3 };  // unit fate this step (atomicMax order)
 
 // ---------------------------------------------------------------- layout
 // Receptor bead (j,k) (1-based) coordinate c lives at

@@ -19,12 +19,12 @@ using namespace kmcd;
 // kernel ids for per-kernel HIP-event timing (kmc_set_timing / kmc_kernel_times)
 enum KId {
   KI_CLASSIFY, KI_BFS, KI_BFS_OVF, KI_PROPOSE, KI_COMPLEX, KI_REC_COUNT, KI_SCAN, KI_REC_SCATTER,
-  KI_RESOLVE0, KI_RESOLVE1, KI_RESOLVE_TAIL, KI_COMMIT, KI_RXN_SCAN, KI_RXN_EXACT, KI_RL_MATCH, KI_CIS_MATCH, KI_DISS_RL,
+  KI_COL_SCAN, KI_COL_EXACT, KI_COL_ROUNDS, KI_COMMIT, KI_RXN_SCAN, KI_RXN_EXACT, KI_RL_MATCH, KI_CIS_MATCH, KI_DISS_RL,
   KI_DISS_CIS, KI_OBSERVE, KI_FINALIZE, KI_N
 };
 static const char* const KNAMES[KI_N] = {
     "k_classify", "k_bfs", "k_bfs_overflow", "k_propose", "k_complex", "k_rec_count", "k_scan",
-    "k_rec_scatter", "k_resolve_r0", "k_resolve_r1", "k_resolve_tail", "k_commit", "k_rxn_scan", "k_rxn_exact",
+    "k_rec_scatter", "k_col_scan", "k_col_exact", "k_col_rounds", "k_commit", "k_rxn_scan", "k_rxn_exact",
     "k_rl_match", "k_cis_match", "k_diss_rl", "k_diss_cis", "k_observe", "k_finalize"};
 #define TRING 64  // steps of event pairs kept in flight
 
@@ -192,15 +192,20 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   rc |= dalloc(s, &d.cx_size, NB);
   rc |= dalloc(s, &d.cx_nb, NB);
   rc |= dalloc(s, &d.members, N);
-  rc |= dalloc(s, &d.units, N);
+  rc |= dalloc(s, &d.pend, N);
   rc |= dalloc(s, &d.overflow, NB);
-  rc |= dalloc(s, &d.wl0, N);
-  rc |= dalloc(s, &d.wl1, N);
+  rc |= dalloc(s, &d.plist, N);
   rc |= dalloc(s, &d.cell_cnt, s->ncell);
   rc |= dalloc(s, &d.cell_start, s->ncell + 1);
   rc |= dalloc(s, &d.block_sums, s->nscan_blocks);
   rc |= dalloc(s, &d.rec_pos, (size_t)2 * N);
   rc |= dalloc(s, &d.rec_id, (size_t)2 * N);
+  rc |= dalloc(s, &d.rec_site, (size_t)2 * N);
+  // collision candidates: ~1 per proposal at the benchmark densities; every
+  // pair of records for small dense systems
+  d.cap_cand = (uint32_t)std::max<uint64_t>(8ull * N, std::min<uint64_t>(4ull * N * N, 1ull << 22));
+  rc |= dalloc(s, &d.cand, d.cap_cand);
+  rc |= dalloc(s, &d.conf, d.cap_cand);
   d.cap_pairs = pow2(std::max<uint32_t>(1u << 16, (uint32_t)N));
   rc |= dalloc(s, &d.pairs, d.cap_pairs);
   rc |= dalloc(s, &d.rfinal, N);
@@ -221,6 +226,10 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   }
   const char* po = getenv("KMC_DEBUG_POISON");
   s->poison = po && *po == '1';
+  // debug: lower the LDS tile capacity so that tiles take the global path
+  const char* tc = getenv("KMC_DEBUG_TCAP");
+  K.tcap = TCAP;
+  if (tc && *tc) K.tcap = std::max(0, std::min(TCAP, atoi(tc)));
   *out = s;
   return KMC_OK;
 }
@@ -387,11 +396,17 @@ static int launch_step(kmc_sim* s) {
     k_scan3<<<s->nscan_blocks, SCAN_T, 0, st>>>(d.cell_start, d.block_sums, s->ncell);
   });
   TIMED(KI_REC_SCATTER, (k_rec_scatter<<<gN, T, 0, st>>>(K, d)));
-  const int gR = (2 * K.N + T - 1) / T;
+  const int gX = std::min(2048, (K.N + T - 1) / T);  // grid-stride kernels over device-sized lists
   const int ntiles = ((K.ncx + TILE - 1) / TILE) * ((K.ncy + TILE - 1) / TILE);
-  TIMED(KI_RESOLVE0, (k_resolve0_tile<<<ntiles, 256, 0, st>>>(K, d)));
-  TIMED(KI_RESOLVE1, (k_resolve<<<gN, T, 0, st>>>(K, d, 0)));
-  TIMED(KI_RESOLVE_TAIL, (k_resolve_tail<<<1, 1024, 0, st>>>(K, d)));
+  TIMED(KI_COL_SCAN, (k_col_scan<<<ntiles, 256, 0, st>>>(K, d)));
+  TIMED(KI_COL_EXACT, (k_col_exact<<<gX, T, 0, st>>>(K, d)));
+  TIMED(KI_COL_ROUNDS, {
+    for (int r = 0; r < 2; ++r) {
+      k_col_round<<<gX, T, 0, st>>>(K, d, r);
+      k_col_units<<<gX, T, 0, st>>>(K, d, r);
+    }
+    k_col_tail<<<1, 1024, 0, st>>>(K, d, 2);
+  });
   TIMED(KI_COMMIT, (k_commit<<<gN, T, 0, st>>>(K, d)));
   if (K.NA > 0) {
     TIMED(KI_RXN_SCAN, (k_rxn_scan_tile<<<ntiles, 256, 0, st>>>(K, d)));
@@ -425,7 +440,12 @@ int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out) {
     int64_t n = std::min(chunk, nsteps - done);
     uint32_t zero = 0;
     HIPCHK(s, hipMemcpyAsync(&s->d.ctl->obs_idx, &zero, sizeof zero, hipMemcpyHostToDevice, s->stream));
-    for (int64_t k = 0; k < n; ++k) launch_step(s);
+    for (int64_t k = 0; k < n; ++k) {
+      // unit-state tags are (step mod 2^30): clear them when the tag wraps
+      if (((s->step_done + k + 1) & 0x3fffffff) == 0)
+        HIPCHK(s, hipMemsetAsync(s->d.ustate, 0, sizeof(uint32_t) * (size_t)s->K.N, s->stream));
+      launch_step(s);
+    }
     HIPCHK(s, hipGetLastError());
     HIPCHK(s, hipMemcpyAsync(s->ctl_host, s->d.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, s->stream));
     if (out)

@@ -35,21 +35,24 @@ struct Dev {
   int32_t* b_int;  // [8][NB]  st1..4 nei1..4
   int32_t* owner;  // [N] key of the unit that moves protein p (0-based)
   uint8_t* ukind;  // [N] unit kind keyed at p
-  uint32_t* ustate;  // [N] (step<<2)|S
+  uint32_t* ustate;  // [N] (step<<2)|S this step; older tag = accepted
   uint32_t* moved;   // [N] step tag (main.cpp:122)
   int32_t* cx_off;   // [NB]
   int32_t* cx_size;  // [NB]
   int32_t* cx_nb;    // [NB] ligands in complex
   int32_t* members;  // [N]
-  int32_t* units;    // [N]
+  uint32_t* pend;    // [N] round tag: unit still waiting (resolution pass C)
   int32_t* overflow; // [NB]
-  int32_t* wl0;      // [N]
-  int32_t* wl1;      // [N]
+  int32_t* plist;    // [N] units with conflict entries
   int32_t* cell_cnt;    // [ncell]
   int32_t* cell_start;  // [ncell+1]
   int32_t* block_sums;  // [scan blocks]
   float4* rec_pos;      // [2N]
-  int2* rec_id;         // [2N]  {pid | isnew<<31, owner key}
+  int2* rec_id;         // [2N]  {pid | st3<<29 | st2<<30 | isnew<<31, owner key}
+  float2* rec_site;     // [2N]  receptor [3][3] site xy (float)
+  int2* cand;           // [cap_cand] collision candidates (proposal record, other record)
+  int2* conf;           // [cap_cand] conflict entries (u, kq | isnew<<31)
+  uint32_t cap_cand;
   int2* pairs;          // [cap_pairs] reaction candidate (receptor, record)
   uint8_t* rfinal;      // [N] 1 if the proposal record is the final position
   uint32_t cap_pairs;
@@ -87,7 +90,7 @@ __device__ __forceinline__ uint32_t state_of(const Dev& d, int key, uint32_t ste
     return S_REJ;
   }
   uint32_t v = ld_state(&d.ustate[key]);
-  return (v >> 2) == (step & 0x3fffffffu) ? (v & 3u) : S_UND;
+  return (v >> 2) == (step & 0x3fffffffu) ? (v & 3u) : S_ACC;  // untouched this step: accepted
 }
 __device__ __forceinline__ void set_state(const Dev& d, int key, uint32_t step, uint32_t s) {
   st_state(&d.ustate[key], ((step & 0x3fffffffu) << 2) | s);
@@ -100,20 +103,6 @@ __device__ __forceinline__ int cell_x(const KParams& P, double x) {
 __device__ __forceinline__ int cell_y(const KParams& P, double y) {
   int c = (int)__builtin_floor((y - P.gy0) / P.cs);
   return c < 0 ? 0 : (c >= P.ncy ? P.ncy - 1 : c);
-}
-
-// ================================================================ step begin
-__global__ void k_begin(Dev d) {
-  Ctl* c = d.ctl;
-  c->n_units = 0;
-  c->n_overflow = 0;
-  c->cx_cursor = 0;
-  c->n_wl[0] = 0;
-  c->n_wl[1] = 0;
-  c->n_rl = 0;
-  c->n_cisc = 0;
-  c->rl = c->mono = c->cis = 0;
-  c->tot_prot = c->tot_clu = c->max_size = 0;
 }
 
 // ================================================================ 1. classify
@@ -904,6 +893,8 @@ __global__ void k_rec_scatter(KParams P, Dev d) {
     int pos = d.cell_start[c] + atomicSub(&d.cell_cnt[c], 1) - 1;  // leaves cell_cnt zeroed
     d.rec_pos[pos] = make_float4((float)x, (float)y, (float)zl, (float)zh);
     d.rec_id[pos] = make_int2(p | st | (w << 31), d.owner[p]);
+    const Beads& B = w ? d.nxt : d.cur;  // cis site [3][3] (reaction prefilter)
+    d.rec_site[pos] = p < NA ? make_float2((float)B.A(p, 3, 3, 0), (float)B.A(p, 3, 3, 1)) : make_float2(0.f, 0.f);
   }
 }
 
@@ -978,161 +969,100 @@ __device__ bool exact_collide(const KParams& P, const Own& o, const Beads& B, in
 __device__ __forceinline__ bool prefilter(bool mA, float mx, float my, float mzl, float mzh, bool qA, float4 r) {
   float dx = r.x - mx, dy = r.y - my;
   float dxy2 = dx * dx + dy * dy;
-  if (mA && qA) {
-    float dz = r.z - mzl;
-    return dxy2 + dz * dz < 42.0f * 42.0f;
-  }
-  if (!mA && !qA) {
-    float dz = r.z - mzl;
-    return dxy2 + dz * dz < 131.5f * 131.5f;
-  }
+  // same kind: centre distance (receptors: z of the lowest domain)
+  float dz = r.z - mzl;
+  bool same = dxy2 + dz * dz < (mA ? 42.0f * 42.0f : 131.5f * 131.5f);
   // receptor axis [zlo, zhi] vs ligand centre
-  float lz, alo, ahi;
-  if (mA) {
-    lz = r.z;
-    alo = mzl;
-    ahi = mzh;
-  } else {
-    lz = mzl;
-    alo = r.z;
-    ahi = r.w;
-  }
-  if (!(dxy2 < 86.5f * 86.5f)) return false;
-  return lz > alo - 86.5f && lz < ahi + 86.5f;
+  float lz = mA ? r.z : mzl, alo = mA ? mzl : r.z, ahi = mA ? mzh : r.w;
+  bool mixed = (dxy2 < 86.5f * 86.5f) & (lz > alo - 86.5f) & (lz < ahi + 86.5f);
+  return mA == qA ? same : mixed;  // branch-free: evaluated in the scans' inner loops
 }
 
-__device__ uint32_t evaluate_unit(const KParams& P, const Dev& d, int u, uint32_t step, const float4* key_ref) {
-  const int NA = P.NA;
-  uint8_t kind = d.ukind[u];
-  int nm;
-  const int* mem = nullptr;
-  int two[2];
-  if (kind == U_COMPLEX) {
-    int lb = u - NA;
-    nm = d.cx_size[lb];
-    mem = d.members + d.cx_off[lb];
-  } else if (kind == U_DIMER) {
-    two[0] = u;
-    two[1] = A_NEI3(d, u) - 1;
-    nm = 2;
-    mem = two;
-  } else {
-    two[0] = u;
-    nm = 1;
-    mem = two;
-  }
-  bool blocked = false;
-  for (int t = 0; t < nm; ++t) {
-    int m = mem[t];
-    const bool mA = m < NA;
-    float mx, my, mzl, mzh;
-    if (key_ref && m == u) {
-      mx = key_ref->x;
-      my = key_ref->y;
-      mzl = key_ref->z;
-      mzh = key_ref->w;
-    } else {
-      double x, y, zl, zh;
-      ref_point(d, d.nxt, m, NA, x, y, zl, zh);
-      mx = (float)x;
-      my = (float)y;
-      mzl = (float)zl;
-      mzh = (float)zh;
-    }
-    // cell of the proposal: from the exact [1][1] (records are binned on it)
-    double ex = mA ? d.nxt.A(m, 1, 1, 0) : d.nxt.B(m - NA, 1, 1, 0);
-    double ey = mA ? d.nxt.A(m, 1, 1, 1) : d.nxt.B(m - NA, 1, 1, 1);
-    int cx = cell_x(P, ex), cy = cell_y(P, ey);
-    Own o;
-    bool loaded = false;
-    for (int yy = cy - 1; yy <= cy + 1; ++yy) {
-      if (yy < 0 || yy >= P.ncy) continue;
-      int x0 = cx > 0 ? cx - 1 : 0, x1 = cx + 1 < P.ncx ? cx + 1 : P.ncx - 1;
-      int r0 = d.cell_start[yy * P.ncx + x0], r1 = d.cell_start[yy * P.ncx + x1 + 1];
-      for (int r = r0; r < r1; ++r) {
-        int2 id = d.rec_id[r];
-        int q = id.x & RID_PID;
-        if (q == m) continue;
-        if (!prefilter(mA, mx, my, mzl, mzh, q < NA, d.rec_pos[r])) continue;
-        bool isnew = id.x < 0;
-        int kq = id.y;
-        bool pending = false;
-        if (kq < 0) {
-          atomicOr(&d.ctl->err, ERR_RESOLVE);
-          continue;
-        }
-        if (kq == u) {
-          if (!isnew) continue;
-        } else if (kq > u) {
-          if (isnew) continue;
-        } else {
-          uint32_t st = state_of(d, kq, step);
-          if (st == S_ACC) {
-            if (!isnew) continue;
-          } else if (st == S_REJ) {
-            if (isnew) continue;
-          } else {
-            pending = true;
-          }
-        }
-        if (!loaded) {
-          load_own(P, d.nxt, m, o);
-          loaded = true;
-        }
-        if (exact_collide(P, o, isnew ? d.nxt : d.cur, q)) {
-          if (!pending) return S_REJ;
-          blocked = true;
-        }
-      }
-    }
-  }
-  return blocked ? S_UND : S_ACC;
+// ---------------------------------------------------------------- emitters
+// Output lists with one global counter: entries are staged in an LDS buffer
+// (slots handed out per wave: one LDS atomic per emitting wave-instruction),
+// and one global atomicAdd per workgroup reserves the output range.  Entries
+// beyond the LDS buffer go straight to global memory.
+#define EBUF 512
+struct WgList {
+  int2 buf[EBUF];
+  uint32_t n;
+  uint32_t base;
+};
+
+// slot for each calling lane (call from the lanes that emit)
+__device__ __forceinline__ uint32_t wave_slot(uint32_t* ctr) {
+  const uint64_t mask = __ballot(1);
+  const int lane = __lane_id();
+  const int leader = __ffsll((unsigned long long)mask) - 1;
+  const uint32_t rank = __popcll(mask & ((1ull << lane) - 1ull));
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(ctr, (uint32_t)__popcll(mask));
+  base = __shfl(base, leader, 64);
+  return base + rank;
 }
 
-// round 0: one thread per record in cell order — the thread holding a unit
-// key's proposal record evaluates that unit, so a wave's lanes scan
-// neighbouring cells (spatially coherent loads)
-__global__ void k_resolve0(KParams P, Dev d) {
-  int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= 2 * P.N) return;
-  int2 id = d.rec_id[r];
-  if (id.x >= 0) return;  // old-position record
-  int u = id.x & RID_PID;
-  if (id.y != u || d.ukind[u] == U_NONE) return;
-  float4 ref = d.rec_pos[r];
-  const uint32_t step = d.ctl->step;
-  uint32_t s = evaluate_unit(P, d, u, step, &ref);
-  if (s == S_UND) {
-    uint32_t pos = atomicAdd(&d.ctl->n_wl[0], 1u);
-    d.wl0[pos] = u;
-  } else {
-    set_state(d, u, step, s);
+__device__ __forceinline__ void wg_list_init(WgList& L) {
+  if (threadIdx.x == 0) L.n = 0;
+  __syncthreads();
+}
+
+__device__ __forceinline__ void wg_emit(WgList& L, int2 v, uint32_t* gctr, int2* gout, uint32_t cap, uint32_t* err) {
+  uint32_t s = wave_slot(&L.n);
+  if (s < EBUF) {
+    L.buf[s] = v;
+    return;
+  }
+  uint32_t pos = wave_slot(gctr);
+  if (pos < cap) gout[pos] = v;
+  else atomicOr(err, ERR_EDGES);
+}
+
+// all threads of the workgroup
+__device__ __forceinline__ void wg_flush(WgList& L, uint32_t* gctr, int2* gout, uint32_t cap, uint32_t* err) {
+  __syncthreads();
+  const uint32_t m = min(L.n, (uint32_t)EBUF);
+  if (threadIdx.x == 0) L.base = m ? atomicAdd(gctr, m) : 0;
+  __syncthreads();
+  const uint32_t base = L.base;
+  for (uint32_t t = threadIdx.x; t < m; t += blockDim.x) {
+    if (base + t < cap) gout[base + t] = L.buf[t];
+    else atomicOr(err, ERR_EDGES);
   }
 }
 
 // ---------------------------------------------------------------- LDS tiles
 // A workgroup owns a TILE×TILE block of cells.  It stages the records of the
-// block plus a one-cell halo into LDS with coalesced row loads (a halo row of
-// cells is one contiguous record range of the cell-sorted array), then every
-// thread scans its records' 3x3 neighbourhoods from LDS.  Only prefilter hits
-// touch global memory (unit state, exact fp64 beads).
+// block plus a one-cell halo into LDS (a halo row of cells is one contiguous
+// range of the cell-sorted record array; all loads are issued up front), then
+// each thread takes interior records and scans their 3x3 cells from LDS.
 #define TILE 16
 #define HALO (TILE + 2)
 #define TCAP 1280
 struct TileLds {
   float4 pos[TCAP];
   int2 id[TCAP];
-  int cstart[HALO][HALO + 1];  // LDS index of each halo cell's first record (+ row end)
-  int g0[HALO];                // global index of each halo row's first record
+  uint16_t cell[TCAP];         // hy * HALO + hx of each staged record
+  int cstart[HALO][HALO + 1];  // LDS index of each halo cell's first record; [hy][HALO] = row end
+  int goff[HALO];              // global record index − LDS index, per halo row
   int n;
-  int overflow;
 };
 
-// returns false if the tile does not fit TCAP (caller falls back to global)
-__device__ bool tile_load(const KParams& P, const Dev& d, int tx, int ty, TileLds& T) {
+// largest i in [0, HALO) with a[i] <= v  (a non-decreasing, a[0] <= v)
+__device__ __forceinline__ int halo_search(const int* a, int stride, int v) {
+  int i = 0;
+#pragma unroll
+  for (int s = 16; s; s >>= 1)
+    if (i + s < HALO && a[(i + s) * stride] <= v) i += s;
+  return i;
+}
+
+// Returns false (uniformly) when the tile holds more than P.tcap records; the
+// caller then takes the global-memory path.  site/fin (reaction scan only):
+// the [3][3] site of each record and whether it is the protein's final position.
+__device__ bool tile_load(const KParams& P, const Dev& d, int tx, int ty, TileLds& T, float2* site, uint8_t* fin) {
   const int cx0 = tx * TILE - 1, cy0 = ty * TILE - 1;
   const int xlo = max(cx0, 0), xhi = min(cx0 + HALO - 1, P.ncx - 1);
-  // 1. raw cell boundaries (global record indices), one per thread
   for (int idx = threadIdx.x; idx < HALO * (HALO + 1); idx += blockDim.x) {
     int hy = idx / (HALO + 1), hx = idx % (HALO + 1);
     int y = cy0 + hy;
@@ -1144,218 +1074,261 @@ __device__ bool tile_load(const KParams& P, const Dev& d, int tx, int ty, TileLd
     T.cstart[hy][hx] = v;
   }
   __syncthreads();
-  // 2. row bases in LDS
-  if (threadIdx.x == 0) {
-    int n = 0;
-    for (int hy = 0; hy < HALO; ++hy) {
-      T.g0[hy] = T.cstart[hy][0];
-      int len = T.cstart[hy][HALO] - T.cstart[hy][0];
-      T.cstart[hy][HALO] = n;  // temporarily: LDS row base
-      n += len;
+  if (threadIdx.x < 64) {  // row lengths -> LDS row bases (wave-0 inclusive scan)
+    int hy = threadIdx.x;
+    int len = hy < HALO ? T.cstart[hy][HALO] - T.cstart[hy][0] : 0;
+    int inc = len;
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+      int t = __shfl_up(inc, o, 64);
+      if (hy >= o) inc += t;
     }
-    T.n = n;
-    T.overflow = n > TCAP;
+    if (hy < HALO) T.goff[hy] = T.cstart[hy][0] - (inc - len);
+    if (hy == HALO - 1) T.n = inc;
   }
   __syncthreads();
   for (int idx = threadIdx.x; idx < HALO * (HALO + 1); idx += blockDim.x) {
     int hy = idx / (HALO + 1), hx = idx % (HALO + 1);
-    if (hx == HALO) continue;
-    T.cstart[hy][hx] = T.cstart[hy][HALO] + (T.cstart[hy][hx] - T.g0[hy]);
+    T.cstart[hy][hx] -= T.goff[hy];
   }
   __syncthreads();
-  if (threadIdx.x < HALO) {  // row end = next row's base
-    int hy = threadIdx.x;
-    T.cstart[hy][HALO] = hy + 1 < HALO ? T.cstart[hy + 1][0] : T.n;
-  }
-  __syncthreads();
-  if (T.overflow) return false;
-  // 3. copy every halo row's contiguous record range
-  for (int hy = 0; hy < HALO; ++hy) {
-    int lo = T.cstart[hy][0], hi = T.cstart[hy][HALO];
-    int g0 = T.g0[hy];
-    for (int t = threadIdx.x; t < hi - lo; t += blockDim.x) {
-      T.pos[lo + t] = d.rec_pos[g0 + t];
-      T.id[lo + t] = d.rec_id[g0 + t];
+  const int n = T.n;
+  if (n > P.tcap) return false;
+  // four records per thread in flight: loads from clamped indices first, then
+  // the LDS stores (keeps the staging arrays in registers)
+  for (int base = 0; base < n; base += 4 * blockDim.x) {
+    float4 p[4];
+    int2 id[4];
+    int hyk[4], g[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      int l = min(base + k * (int)blockDim.x + (int)threadIdx.x, n - 1);
+      hyk[k] = halo_search(&T.cstart[0][0], HALO + 1, l);
+      g[k] = l + T.goff[hyk[k]];
+      p[k] = d.rec_pos[g[k]];
+      id[k] = d.rec_id[g[k]];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      int l = base + k * (int)blockDim.x + (int)threadIdx.x;
+      if (l < n) {
+        int hx = halo_search(&T.cstart[hyk[k]][0], 1, l);
+        T.pos[l] = p[k];
+        T.id[l] = id[k];
+        T.cell[l] = (uint16_t)(hyk[k] * HALO + hx);
+        if (site) {
+          site[l] = d.rec_site[g[k]];
+          fin[l] = (id[k].x < 0) == (d.rfinal[id[k].x & RID_PID] != 0);
+        }
+      }
     }
   }
   __syncthreads();
   return true;
 }
 
-// interior records of the tile (halo rows 1..TILE, cells 1..TILE) as one flat
-// index space: thread t takes the t-th interior record of the tile
-__device__ __forceinline__ int interior_count(const TileLds& T) {
-  int n = 0;
-  for (int hy = 1; hy <= TILE; ++hy) n += T.cstart[hy][TILE + 1] - T.cstart[hy][1];
-  return n;
-}
-__device__ __forceinline__ int interior_record(const TileLds& T, int t, int* hy_out, int* hx_out) {
-  int hy = 1;
-  for (;; ++hy) {
-    int len = T.cstart[hy][TILE + 1] - T.cstart[hy][1];
-    if (t < len) break;
-    t -= len;
-  }
-  int r = T.cstart[hy][1] + t;
-  int hx = 1;
-  while (T.cstart[hy][hx + 1] <= r) ++hx;
-  *hy_out = hy;
-  *hx_out = hx;
-  return r;
+// ---------------------------------------------------------------- 4a. scan
+// Pass A: every proposal record (member m of unit u = its owner) is checked
+// against the records of its 3x3 cells.  The filters that do not depend on
+// any unit's fate are applied here (main.cpp:640-664 visits R_new, i.e. the
+// proposals of earlier units and the old positions of later ones):
+//   owner kq == u : only the unit's other proposal records
+//   owner kq >  u : only old-position records
+//   owner kq <  u : both (which one counts is decided by kq's fate, pass C)
+// A record passing them and the conservative prefilter is a candidate.
+__device__ __forceinline__ void col_emit(const Dev& d, WgList& L, int rs, int rg) {
+  wg_emit(L, make_int2(rs, rg), &d.ctl->n_cand, d.cand, d.cap_cand, &d.ctl->err);
 }
 
-// single-member unit u (free receptor / free ligand) whose proposal record is
-// at halo cell (hx, hy) of the tile
-__device__ uint32_t evaluate_single_lds(const KParams& P, const Dev& d, const TileLds& T, int u, float4 me, int hx,
-                                        int hy, uint32_t step) {
+// pos/ids: record source (LDS or global); rows k=0..2: [r0[k], r1[k]) with
+// global index = r + goff[k].  The three row ranges are walked as one loop and
+// the filters are branch-free (lanes of a wave stay converged).
+__device__ __forceinline__ void col_scan_rec(const KParams& P, const Dev& d, WgList& L, const float4* pos,
+                                             const int2* ids, const int* r0, const int* r1, const int* goff, int rs,
+                                             int2 me, float4 mp) {
   const int NA = P.NA;
-  const bool mA = u < NA;
-  bool blocked = false, loaded = false;
-  Own o;
-  for (int yy = hy - 1; yy <= hy + 1; ++yy) {
-    int r0 = T.cstart[yy][hx - 1], r1 = T.cstart[yy][hx + 2];
-    for (int r = r0; r < r1; ++r) {
-      int2 id = T.id[r];
-      int q = id.x & RID_PID;
-      if (q == u) continue;
-      if (!prefilter(mA, me.x, me.y, me.z, me.w, q < NA, T.pos[r])) continue;
-      bool isnew = id.x < 0;
-      int kq = id.y;
-      bool pending = false;
-      if (kq < 0) {
-        atomicOr(&d.ctl->err, ERR_RESOLVE);
-        continue;
-      }
-      if (kq > u) {
-        if (isnew) continue;
-      } else {  // kq < u (a single-member unit owns only itself)
-        uint32_t st = state_of(d, kq, step);
-        if (st == S_ACC) {
-          if (!isnew) continue;
-        } else if (st == S_REJ) {
-          if (isnew) continue;
-        } else {
-          pending = true;
-        }
-      }
-      if (!loaded) {
-        load_own(P, d.nxt, u, o);
-        loaded = true;
-      }
-      if (exact_collide(P, o, isnew ? d.nxt : d.cur, q)) {
-        if (!pending) return S_REJ;
-        blocked = true;
-      }
-    }
-  }
-  return blocked ? S_UND : S_ACC;
-}
-
-__device__ __forceinline__ void resolve_emit(const Dev& d, int u, uint32_t step, uint32_t s) {
-  if (s == S_UND) {
-    uint32_t pos = atomicAdd(&d.ctl->n_wl[0], 1u);
-    d.wl0[pos] = u;
-  } else {
-    set_state(d, u, step, s);
-  }
-}
-
-// round 0, tiled: every unit keyed at a proposal record inside the tile
-__global__ void __launch_bounds__(256) k_resolve0_tile(KParams P, Dev d) {
-  __shared__ TileLds T;
-  const int ntx = (P.ncx + TILE - 1) / TILE;
-  const int tx = blockIdx.x % ntx, ty = blockIdx.x / ntx;
-  const uint32_t step = d.ctl->step;
-  const int cx0 = tx * TILE - 1, cy0 = ty * TILE - 1;
-  if (!tile_load(P, d, tx, ty, T)) {
-    // dense tile: scan the block's interior records from global memory
-    for (int hy = 1; hy <= TILE; ++hy) {
-      int y = cy0 + hy;
-      if (y < 0 || y >= P.ncy) continue;
-      int xlo = max(cx0 + 1, 0), xhi = min(cx0 + TILE, P.ncx - 1);
-      if (xlo > xhi) continue;
-      int r0 = d.cell_start[y * P.ncx + xlo], r1 = d.cell_start[y * P.ncx + xhi + 1];
-      for (int r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
-        int2 id = d.rec_id[r];
-        if (id.x >= 0) continue;
-        int u = id.x & RID_PID;
-        if (id.y != u || d.ukind[u] == U_NONE) continue;
-        float4 ref = d.rec_pos[r];
-        resolve_emit(d, u, step, evaluate_unit(P, d, u, step, &ref));
-      }
-    }
+  const int m = me.x & RID_PID, u = me.y;
+  if (u < 0) {
+    atomicOr(&d.ctl->err, ERR_RESOLVE);
     return;
   }
-  const int nint = interior_count(T);
-  for (int t = threadIdx.x; t < nint; t += blockDim.x) {
-    int hy, hx;
-    int r = interior_record(T, t, &hy, &hx);
-    int2 id = T.id[r];
-    if (id.x >= 0) continue;  // old-position record
-    int u = id.x & RID_PID;
-    if (id.y != u) continue;
-    uint8_t kind = d.ukind[u];
-    if (kind == U_NONE) continue;
-    float4 me = T.pos[r];
-    uint32_t s;
-    if (kind == U_FREE_A || kind == U_FREE_B) s = evaluate_single_lds(P, d, T, u, me, hx, hy, step);
-    else s = evaluate_unit(P, d, u, step, &me);  // dimer / complex: members anywhere
-    resolve_emit(d, u, step, s);
+  const bool mA = m < NA;
+  const int l0 = r1[0] - r0[0], l01 = l0 + r1[1] - r0[1], tot = l01 + r1[2] - r0[2];
+  for (int t = 0; t < tot; ++t) {
+    const bool k0 = t < l0, k1 = t < l01;
+    const int r = k0 ? r0[0] + t : (k1 ? r0[1] + (t - l0) : r0[2] + (t - l01));
+    const int2 id = ids[r];
+    const float4 rp = pos[r];
+    const int q = id.x & RID_PID, kq = id.y;
+    const bool isnew = id.x < 0;
+    const bool own_ok = kq == u ? isnew : (kq > u ? !isnew : true);
+    if ((q != m) & own_ok & prefilter(mA, mp.x, mp.y, mp.z, mp.w, q < NA, rp)) {
+      if (kq < 0) atomicOr(&d.ctl->err, ERR_RESOLVE);
+      else col_emit(d, L, rs, r + (k0 ? goff[0] : (k1 ? goff[1] : goff[2])));
+    }
   }
 }
 
-// round 1: the units round 0 left undecided
-__global__ void k_resolve(KParams P, Dev d, int src) {
-  const uint32_t step = d.ctl->step;
-  uint32_t n = d.ctl->n_wl[src];
-  const int32_t* list = src == 0 ? d.wl0 : d.wl1;
-  int32_t* dst = src == 0 ? d.wl1 : d.wl0;
-  uint32_t* ndst = &d.ctl->n_wl[src ^ 1];
+__global__ void __launch_bounds__(256) k_col_scan(KParams P, Dev d) {
+  __shared__ TileLds T;
+  __shared__ WgList L;
+  __shared__ uint16_t work[TCAP];  // the tile's interior proposal records
+  __shared__ uint32_t nwork;
+  const int ntx = (P.ncx + TILE - 1) / TILE;
+  const int tx = blockIdx.x % ntx, ty = blockIdx.x / ntx;
+  if (threadIdx.x == 0) nwork = 0;
+  wg_list_init(L);
+  if (tile_load(P, d, tx, ty, T, nullptr, nullptr)) {
+    for (int l = threadIdx.x; l < T.n; l += blockDim.x) {
+      int c = T.cell[l];
+      int hy = c / HALO, hx = c - hy * HALO;
+      if (hx >= 1 && hx <= TILE && hy >= 1 && hy <= TILE && T.id[l].x < 0) work[wave_slot(&nwork)] = (uint16_t)l;
+    }
+    __syncthreads();
+    const int nw = nwork;
+    for (int w = threadIdx.x; w < nw; w += blockDim.x) {
+      const int l = work[w];
+      const int c = T.cell[l];
+      const int hy = c / HALO, hx = c - hy * HALO;
+      int r0[3], r1[3], go[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        r0[k] = T.cstart[hy - 1 + k][hx - 1];
+        r1[k] = T.cstart[hy - 1 + k][hx + 2];
+        go[k] = T.goff[hy - 1 + k];
+      }
+      col_scan_rec(P, d, L, T.pos, T.id, r0, r1, go, l + T.goff[hy], T.id[l], T.pos[l]);
+    }
+    wg_flush(L, &d.ctl->n_cand, d.cand, d.cap_cand, &d.ctl->err);
+    return;
+  }
+  // dense tile: one thread per interior cell, records from global memory
+  for (int c = threadIdx.x; c < TILE * TILE; c += blockDim.x) {
+    int x = tx * TILE + c % TILE, y = ty * TILE + c / TILE;
+    if (x >= P.ncx || y >= P.ncy) continue;
+    int r0[3], r1[3], go[3] = {0, 0, 0};
+    int x0 = max(x - 1, 0), x1 = min(x + 1, P.ncx - 1);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      int yy = y - 1 + k;
+      bool ok = yy >= 0 && yy < P.ncy;
+      r0[k] = ok ? d.cell_start[yy * P.ncx + x0] : 0;
+      r1[k] = ok ? d.cell_start[yy * P.ncx + x1 + 1] : 0;
+    }
+    int s0 = d.cell_start[y * P.ncx + x], s1 = d.cell_start[y * P.ncx + x + 1];
+    for (int r = s0; r < s1; ++r) {
+      int2 me = d.rec_id[r];
+      if (me.x >= 0) continue;
+      col_scan_rec(P, d, L, d.rec_pos, d.rec_id, r0, r1, go, r, me, d.rec_pos[r]);
+    }
+  }
+  wg_flush(L, &d.ctl->n_cand, d.cand, d.cap_cand, &d.ctl->err);
+}
+
+// ---------------------------------------------------------------- 4b. exact
+// Pass B: exact fp64 overlap test of each candidate (main.cpp:640-664,
+// 1798-1826).  A collision with a record whose relevance is already known
+// (own unit, or a later unit's old position) rejects u outright; one with an
+// earlier unit's record becomes a conflict entry (u, kq, isnew) for pass C.
+// Unit states this step: untouched = accepted, S_PEND, S_REJ (atomicMax).
+__global__ void k_col_exact(KParams P, Dev d) {
+  const uint32_t tag = (d.ctl->step & 0x3fffffffu) << 2;
+  uint32_t n = d.ctl->n_cand;
+  if (n > d.cap_cand) n = d.cap_cand;
   for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
-    int u = list[t];
-    uint32_t s = evaluate_unit(P, d, u, step, nullptr);
-    if (s == S_UND) {
-      uint32_t pos = atomicAdd(ndst, 1u);
-      dst[pos] = u;
-    } else {
-      set_state(d, u, step, s);
+    int2 c = d.cand[t];
+    int2 a = d.rec_id[c.x], b = d.rec_id[c.y];
+    int m = a.x & RID_PID, u = a.y, q = b.x & RID_PID, kq = b.y;
+    bool isnew = b.x < 0;
+    Own o;
+    load_own(P, d.nxt, m, o);
+    if (!exact_collide(P, o, isnew ? d.nxt : d.cur, q)) continue;
+    if (kq >= u) {
+      atomicMax(&d.ustate[u], tag | S_REJ);
+      continue;
     }
+    uint32_t old = atomicMax(&d.ustate[u], tag | S_PEND);
+    if ((old & ~3u) != tag) {
+      uint32_t pos = atomicAdd(&d.ctl->n_plist, 1u);
+      d.plist[pos] = u;  // at most one entry per unit: capacity N
+    } else if ((old & 3u) == S_REJ) {
+      continue;
+    }
+    uint32_t pos = atomicAdd(&d.ctl->n_conf, 1u);
+    if (pos < d.cap_cand) d.conf[pos] = make_int2(u, kq | (isnew ? (int)0x80000000 : 0));
+    else atomicOr(&d.ctl->err, ERR_EDGES);
   }
 }
 
-// single-workgroup tail: iterate until every unit is decided; the lowest
-// undecided key always decides, so this terminates
-__global__ void __launch_bounds__(1024) k_resolve_tail(KParams P, Dev d) {
-  __shared__ uint32_t n_next, n_cur;
-  __shared__ int flip;
+// ---------------------------------------------------------------- 4c. rounds
+// Pass C: Gauss–Seidel resolution on the conflict entries.  Entry (u, kq,
+// new): once kq is decided, the collision counts iff kq accepted and the
+// record is its proposal, or kq was rejected and the record is its old
+// position.  A unit is accepted when none of its entries counts or waits.
+// Only sound deductions are made, in any order, so the outcome is the
+// sequential one; the lowest pending key can always decide, so it ends.
+__device__ __forceinline__ uint32_t round_tag(uint32_t step, int round) { return step * 64u + (uint32_t)round; }
+
+__device__ __forceinline__ void conf_entry(const Dev& d, int2 e, uint32_t step, uint32_t rt) {
+  int u = e.x, kq = e.y & 0x7fffffff;
+  bool isnew = e.y < 0;
+  if (state_of(d, u, step) != S_PEND) return;
+  uint32_t sk = state_of(d, kq, step);
+  if (sk == S_PEND) st_state(&d.pend[u], rt);
+  else if ((sk == S_ACC) == isnew) atomicMax(&d.ustate[u], ((step & 0x3fffffffu) << 2) | S_REJ);
+}
+
+// returns 1 if u is still pending after this round
+__device__ __forceinline__ int conf_unit(const Dev& d, int u, uint32_t step, uint32_t rt) {
+  if (state_of(d, u, step) != S_PEND) return 0;
+  if (ld_state(&d.pend[u]) == rt) return 1;
+  set_state(d, u, step, S_ACC);
+  return 0;
+}
+
+__global__ void k_col_round(KParams P, Dev d, int round) {
   const uint32_t step = d.ctl->step;
-  if (threadIdx.x == 0) {
-    n_cur = d.ctl->n_wl[1];
-    flip = 0;
-  }
-  __syncthreads();
-  uint32_t guard = 0;
-  while (n_cur > 0) {
-    if (threadIdx.x == 0) n_next = 0;
+  const uint32_t rt = round_tag(step, round);
+  uint32_t n = d.ctl->n_conf;
+  if (n > d.cap_cand) n = d.cap_cand;
+  if (blockIdx.x == 0 && threadIdx.x == 0) d.ctl->n_pend = 0;
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x)
+    conf_entry(d, d.conf[t], step, rt);
+}
+
+__global__ void k_col_units(KParams P, Dev d, int round) {
+  const uint32_t step = d.ctl->step;
+  const uint32_t rt = round_tag(step, round);
+  uint32_t n = d.ctl->n_plist;
+  int pend = 0;
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x)
+    pend += conf_unit(d, d.plist[t], step, rt);
+  if (pend) atomicAdd(&d.ctl->n_pend, (uint32_t)pend);
+}
+
+// single workgroup: the remaining rounds, until nothing is pending
+__global__ void __launch_bounds__(1024) k_col_tail(KParams P, Dev d, int round0) {
+  __shared__ uint32_t npend;
+  if (d.ctl->n_pend == 0) return;
+  const uint32_t step = d.ctl->step;
+  uint32_t n = d.ctl->n_conf;
+  if (n > d.cap_cand) n = d.cap_cand;
+  const uint32_t nu = d.ctl->n_plist;
+  for (int round = round0;; ++round) {
+    const uint32_t rt = round_tag(step, round);
+    if (threadIdx.x == 0) npend = 0;
+    for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) conf_entry(d, d.conf[t], step, rt);
     __syncthreads();
-    int32_t* src = flip ? d.wl0 : d.wl1;
-    int32_t* dst = flip ? d.wl1 : d.wl0;
-    for (uint32_t t = threadIdx.x; t < n_cur; t += blockDim.x) {
-      int u = src[t];
-      uint32_t s = evaluate_unit(P, d, u, step, nullptr);
-      if (s == S_UND) dst[atomicAdd(&n_next, 1u)] = u;
-      else set_state(d, u, step, s);
-    }
+    int pend = 0;
+    for (uint32_t t = threadIdx.x; t < nu; t += blockDim.x) pend += conf_unit(d, d.plist[t], step, rt);
+    if (pend) atomicAdd(&npend, (uint32_t)pend);
     __syncthreads();
-    if (threadIdx.x == 0) {
-      n_cur = n_next;
-      flip ^= 1;
-    }
-    __syncthreads();
-    if (++guard > (uint32_t)P.N + 2) {
+    if (npend == 0) break;
+    if ((uint32_t)(round - round0) > nu + 2) {
       if (threadIdx.x == 0) atomicOr(&d.ctl->err, ERR_RESOLVE);
       break;
     }
+    __syncthreads();
   }
 }
 
@@ -1384,169 +1357,140 @@ __device__ __forceinline__ bool record_final(const Dev& d, int2 id) {
   return (id.x < 0) == (d.rfinal[id.x & RID_PID] != 0);
 }
 
-// Reaction candidates, pass 1: one thread per record in cell order; the
-// final-position record of a receptor that can still react scans the final
-// records of its 3x3 cells with conservative single-precision prefilters
-// (R–L: ligand centre within reach of the [3][2] site; cis: the two [3][3]
-// sites within 16 Å) and emits (receptor, partner) pairs.  Light on
-// registers; the exact gates run in pass 2 over the (few) pairs.
-__global__ void k_rxn_scan(KParams P, Dev d) {
+// Reaction candidates, pass 1 (tiled): the final-position record of every
+// receptor that can still react scans the final records of its 3x3 cells
+// with conservative single-precision prefilters (R–L: ligand centre within
+// reach of the [3][2] site; cis: the two [3][3] sites within 16 Å) and emits
+// (receptor, partner) pairs; the exact gates run in pass 2.  Record sites
+// and final flags are staged in LDS with the tile.
+__device__ __forceinline__ void rxn_emit(const Dev& d, WgList& L, int i, int q) {
+  wg_emit(L, make_int2(i, q), &d.ctl->n_pairs, d.pairs, d.cap_pairs, &d.ctl->err);
+}
+
+// one receptor record; LDS: record r's site/final from site[]/fin[],
+// global: from rec_site / rfinal
+template <bool LDS>
+__device__ __forceinline__ void rxn_scan_rec(const KParams& P, const Dev& d, WgList& L, const float4* pos,
+                                             const int2* ids,
+                                             const float2* site, const uint8_t* fin, const int* r0, const int* r1,
+                                             int2 me, float4 mp, float2 ms) {
   const int NA = P.NA, NB = P.NB;
-  int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= 2 * P.N) return;
-  int2 me = d.rec_id[r];
-  int i = me.x & RID_PID;
-  if (i >= NA) return;
-  bool want_rl = !(me.x & RID_ST2) && NB > 0;
-  bool want_cis = !(me.x & RID_ST3);
-  if (!want_rl && !want_cis) return;
-  if (!record_final(d, me)) return;
-  const Beads& N = d.nxt;
-  float4 mp = d.rec_pos[r];
-  float fx = mp.x, fy = mp.y, fzl = mp.z, fzh = mp.w;
-  float sx = 0, sy = 0;
-  bool have_site = false;
-  double ax = N.A(i, 1, 1, 0), ay = N.A(i, 1, 1, 1);
-  int cx = cell_x(P, ax), cy = cell_y(P, ay);
-  for (int yy = cy - 1; yy <= cy + 1; ++yy) {
-    if (yy < 0 || yy >= P.ncy) continue;
-    int x0 = cx > 0 ? cx - 1 : 0, x1 = cx + 1 < P.ncx ? cx + 1 : P.ncx - 1;
-    int r0 = d.cell_start[yy * P.ncx + x0], r1 = d.cell_start[yy * P.ncx + x1 + 1];
-    for (int rr = r0; rr < r1; ++rr) {
-      int2 id = d.rec_id[rr];
+  const int i = me.x & RID_PID;
+  const bool want_rl = !(me.x & RID_ST2) && NB > 0;
+  const bool want_cis = !(me.x & RID_ST3);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    for (int r = r0[k]; r < r1[k]; ++r) {
+      int2 id = ids[r];
       int q = id.x & RID_PID;
       if (q == i) continue;
-      float4 rp = d.rec_pos[rr];
-      float dx = rp.x - fx, dy = rp.y - fy;
+      float4 rp = pos[r];
+      float dx = rp.x - mp.x, dy = rp.y - mp.y;
       float dxy2 = dx * dx + dy * dy;
       if (q >= NA) {
         if (!want_rl) continue;
-        if (!(dxy2 < 105.0f * 105.0f) || !(rp.z > fzl - 85.0f && rp.z < fzh + 85.0f)) continue;
+        if (!(dxy2 < 105.0f * 105.0f) || !(rp.z > mp.z - 85.0f && rp.z < mp.w + 85.0f)) continue;
       } else {
         if (!want_cis || (id.x & RID_ST3)) continue;
         if (!(dxy2 < 57.0f * 57.0f)) continue;
-        float gap = fmaxf(fmaxf(rp.z - fzh, fzl - rp.w), 0.0f);
+        float gap = fmaxf(fmaxf(rp.z - mp.w, mp.z - rp.w), 0.0f);
         if (!(gap < 16.0f)) continue;
-        if (!have_site) {
-          sx = (float)N.A(i, 3, 3, 0);
-          sy = (float)N.A(i, 3, 3, 1);
-          have_site = true;
-        }
-        float tx = (float)N.A(q, 3, 3, 0) - sx, ty = (float)N.A(q, 3, 3, 1) - sy;
+        float2 qs = LDS ? site[r] : d.rec_site[r];
+        float tx = qs.x - ms.x, ty = qs.y - ms.y;
         if (!(tx * tx + ty * ty < 16.0f * 16.0f)) continue;
       }
-      if (!record_final(d, id)) continue;
-      uint32_t pos = atomicAdd(&d.ctl->n_pairs, 1u);
-      if (pos < d.cap_pairs) d.pairs[pos] = make_int2(i, q);
-      else atomicOr(&d.ctl->err, ERR_EDGES);
+      bool f = LDS ? fin[r] != 0 : record_final(d, id);
+      if (!f) continue;
+      rxn_emit(d, L, i, q);
     }
   }
 }
 
-// reaction scan, tiled: final records of receptors inside the tile
-__device__ void rxn_scan_one(const KParams& P, const Dev& d, const TileLds* T, int i, int2 me, float4 mp, int hx,
-                             int hy, int gcx, int gcy) {
+__device__ __forceinline__ void rxn_scan_lds(const KParams& P, const Dev& d, WgList& L, const TileLds& T,
+                                             const float2* site, const uint8_t* fin, const int* r0, const int* r1,
+                                             int2 me, float4 mp, float2 ms) {
   const int NA = P.NA, NB = P.NB;
-  const Beads& N = d.nxt;
-  bool want_rl = !(me.x & RID_ST2) && NB > 0;
-  bool want_cis = !(me.x & RID_ST3);
-  float fx = mp.x, fy = mp.y, fzl = mp.z, fzh = mp.w;
-  float sx = 0, sy = 0;
-  bool have_site = false;
-  for (int dy = -1; dy <= 1; ++dy) {
-    int r0, r1;
-    if (T) {
-      r0 = T->cstart[hy + dy][hx - 1];
-      r1 = T->cstart[hy + dy][hx + 2];
-    } else {
-      int yy = gcy + dy;
-      if (yy < 0 || yy >= P.ncy) continue;
-      int x0 = gcx > 0 ? gcx - 1 : 0, x1 = gcx + 1 < P.ncx ? gcx + 1 : P.ncx - 1;
-      r0 = d.cell_start[yy * P.ncx + x0];
-      r1 = d.cell_start[yy * P.ncx + x1 + 1];
-    }
-    for (int rr = r0; rr < r1; ++rr) {
-      int2 id = T ? T->id[rr] : d.rec_id[rr];
-      int q = id.x & RID_PID;
-      if (q == i) continue;
-      float4 rp = T ? T->pos[rr] : d.rec_pos[rr];
-      float dx = rp.x - fx, dy2 = rp.y - fy;
-      float dxy2 = dx * dx + dy2 * dy2;
-      if (q >= NA) {
-        if (!want_rl) continue;
-        if (!(dxy2 < 105.0f * 105.0f) || !(rp.z > fzl - 85.0f && rp.z < fzh + 85.0f)) continue;
-      } else {
-        if (!want_cis || (id.x & RID_ST3)) continue;
-        if (!(dxy2 < 57.0f * 57.0f)) continue;
-        float gap = fmaxf(fmaxf(rp.z - fzh, fzl - rp.w), 0.0f);
-        if (!(gap < 16.0f)) continue;
-        if (!have_site) {
-          sx = (float)N.A(i, 3, 3, 0);
-          sy = (float)N.A(i, 3, 3, 1);
-          have_site = true;
-        }
-        float tx = (float)N.A(q, 3, 3, 0) - sx, ty = (float)N.A(q, 3, 3, 1) - sy;
-        if (!(tx * tx + ty * ty < 16.0f * 16.0f)) continue;
-      }
-      if (!record_final(d, id)) continue;
-      uint32_t pos = atomicAdd(&d.ctl->n_pairs, 1u);
-      if (pos < d.cap_pairs) d.pairs[pos] = make_int2(i, q);
-      else atomicOr(&d.ctl->err, ERR_EDGES);
-    }
+  const int i = me.x & RID_PID;
+  const bool want_rl = !(me.x & RID_ST2) && NB > 0;
+  const bool want_cis = !(me.x & RID_ST3);
+  const int l0 = r1[0] - r0[0], l01 = l0 + r1[1] - r0[1], tot = l01 + r1[2] - r0[2];
+  for (int t = 0; t < tot; ++t) {
+    const int r = t < l0 ? r0[0] + t : (t < l01 ? r0[1] + (t - l0) : r0[2] + (t - l01));
+    const int2 id = T.id[r];
+    const float4 rp = T.pos[r];
+    const float2 qs = site[r];
+    const int q = id.x & RID_PID;
+    const bool isB = q >= NA;
+    const float dx = rp.x - mp.x, dy = rp.y - mp.y;
+    const float dxy2 = dx * dx + dy * dy;
+    const bool rl_ok = isB & want_rl & (dxy2 < 105.0f * 105.0f) & (rp.z > mp.z - 85.0f) & (rp.z < mp.w + 85.0f);
+    const float gap = fmaxf(fmaxf(rp.z - mp.w, mp.z - rp.w), 0.0f);
+    const float tx = qs.x - ms.x, ty = qs.y - ms.y;
+    const bool cis_ok = !isB & want_cis & !(id.x & RID_ST3) & (dxy2 < 57.0f * 57.0f) & (gap < 16.0f) &
+                        (tx * tx + ty * ty < 16.0f * 16.0f);
+    if ((q != i) & (rl_ok | cis_ok) & (fin[r] != 0)) rxn_emit(d, L, i, q);
   }
 }
 
 __global__ void __launch_bounds__(256) k_rxn_scan_tile(KParams P, Dev d) {
   __shared__ TileLds T;
+  __shared__ float2 site[TCAP];
+  __shared__ uint8_t fin[TCAP];
+  __shared__ WgList L;
+  __shared__ uint16_t work[TCAP];  // the tile's interior final receptor records that can react
+  __shared__ uint32_t nwork;
   const int ntx = (P.ncx + TILE - 1) / TILE;
   const int tx = blockIdx.x % ntx, ty = blockIdx.x / ntx;
-  const int cx0 = tx * TILE - 1, cy0 = ty * TILE - 1;
   const int NA = P.NA;
-  bool lds = tile_load(P, d, tx, ty, T);
-  if (lds) {
-    const int nint = interior_count(T);
-    for (int t = threadIdx.x; t < nint; t += blockDim.x) {
-      int hy, hx;
-      int r = interior_record(T, t, &hy, &hx);
-      int2 me = T.id[r];
-      int i = me.x & RID_PID;
-      if (i >= NA) continue;
-      if ((me.x & RID_ST2) && (me.x & RID_ST3)) continue;
-      if (!record_final(d, me)) continue;
-      rxn_scan_one(P, d, &T, i, me, T.pos[r], hx, hy, 0, 0);
+  if (threadIdx.x == 0) nwork = 0;
+  wg_list_init(L);
+  if (tile_load(P, d, tx, ty, T, site, fin)) {
+    for (int l = threadIdx.x; l < T.n; l += blockDim.x) {
+      int c = T.cell[l];
+      int hy = c / HALO, hx = c - hy * HALO;
+      int2 me = T.id[l];
+      if (hx >= 1 && hx <= TILE && hy >= 1 && hy <= TILE && (me.x & RID_PID) < NA &&
+          !((me.x & RID_ST2) && (me.x & RID_ST3)) && fin[l])
+        work[wave_slot(&nwork)] = (uint16_t)l;
     }
+    __syncthreads();
+    const int nw = nwork;
+    for (int w = threadIdx.x; w < nw; w += blockDim.x) {
+      const int l = work[w];
+      const int c = T.cell[l];
+      const int hy = c / HALO, hx = c - hy * HALO;
+      int r0[3], r1[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        r0[k] = T.cstart[hy - 1 + k][hx - 1];
+        r1[k] = T.cstart[hy - 1 + k][hx + 2];
+      }
+      rxn_scan_lds(P, d, L, T, site, fin, r0, r1, T.id[l], T.pos[l], site[l]);
+    }
+    wg_flush(L, &d.ctl->n_pairs, d.pairs, d.cap_pairs, &d.ctl->err);
     return;
   }
-  for (int hy = 1; hy <= TILE; ++hy) {
-    int y = cy0 + hy;
-    if (y < 0 || y >= P.ncy) continue;
-    int r0, r1;
-    if (lds) {
-      r0 = T.cstart[hy][1];
-      r1 = T.cstart[hy][TILE + 1];
-    } else {
-      int xlo = max(cx0 + 1, 0), xhi = min(cx0 + TILE, P.ncx - 1);
-      if (xlo > xhi) continue;
-      r0 = d.cell_start[y * P.ncx + xlo];
-      r1 = d.cell_start[y * P.ncx + xhi + 1];
+  for (int c = threadIdx.x; c < TILE * TILE; c += blockDim.x) {
+    int x = tx * TILE + c % TILE, y = ty * TILE + c / TILE;
+    if (x >= P.ncx || y >= P.ncy) continue;
+    int r0[3], r1[3];
+    int x0 = max(x - 1, 0), x1 = min(x + 1, P.ncx - 1);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      int yy = y - 1 + k;
+      bool ok = yy >= 0 && yy < P.ncy;
+      r0[k] = ok ? d.cell_start[yy * P.ncx + x0] : 0;
+      r1[k] = ok ? d.cell_start[yy * P.ncx + x1 + 1] : 0;
     }
-    for (int r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
-      int2 me = lds ? T.id[r] : d.rec_id[r];
-      int i = me.x & RID_PID;
-      if (i >= NA) continue;
-      if ((me.x & RID_ST2) && (me.x & RID_ST3)) continue;
-      if (!record_final(d, me)) continue;
-      float4 mp = lds ? T.pos[r] : d.rec_pos[r];
-      if (lds) {
-        int hx = 1;
-        while (T.cstart[hy][hx + 1] <= r) ++hx;
-        rxn_scan_one(P, d, &T, i, me, mp, hx, hy, 0, 0);
-      } else {
-        double ax = d.nxt.A(i, 1, 1, 0), ay = d.nxt.A(i, 1, 1, 1);
-        rxn_scan_one(P, d, nullptr, i, me, mp, 0, 0, cell_x(P, ax), cell_y(P, ay));
-      }
+    int s0 = d.cell_start[y * P.ncx + x], s1 = d.cell_start[y * P.ncx + x + 1];
+    for (int r = s0; r < s1; ++r) {
+      int2 me = d.rec_id[r];
+      if ((me.x & RID_PID) >= NA || ((me.x & RID_ST2) && (me.x & RID_ST3)) || !record_final(d, me)) continue;
+      rxn_scan_rec<false>(P, d, L, d.rec_pos, d.rec_id, nullptr, nullptr, r0, r1, me, d.rec_pos[r],
+                          d.rec_site[r]);
     }
   }
+  wg_flush(L, &d.ctl->n_pairs, d.pairs, d.cap_pairs, &d.ctl->err);
 }
 
 // Reaction candidates, pass 2: exact R–L association gates (main.cpp:1880-1921)
@@ -1897,11 +1841,9 @@ __global__ void k_finalize(KParams P, Dev d, double time_step) {
   c->obs_idx = c->obs_idx + 1;
   c->step = c->step + 1;
   // per-step counters for the next step (the former k_begin)
-  c->n_units = 0;
   c->n_overflow = 0;
   c->cx_cursor = 0;
-  c->n_wl[0] = 0;
-  c->n_wl[1] = 0;
+  c->n_cand = c->n_conf = c->n_plist = c->n_pend = 0;
   c->n_rl = 0;
   c->n_cisc = 0;
   c->n_pairs = 0;

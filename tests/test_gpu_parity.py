@@ -92,6 +92,22 @@ def test_poisoned_rnew_dense(monkeypatch):
     assert engine.state_hash(p, sim.get_state()) == o.hash()
 
 
+@pytest.mark.parametrize("tcap", [0, 24])
+def test_global_tile_path_dense(monkeypatch, tcap):
+    # LDS tile capacity lowered: every (tcap=0) or most (24) tiles take the
+    # global-memory scan path of the collision and reaction scans
+    monkeypatch.setenv("KMC_DEBUG_TCAP", str(tcap))
+    p = params(seed=23, **DENSE)
+    o = O.Oracle(p)
+    o.init_placement()
+    sim = engine.Simulation(p)
+    sim.set_state(o.get_state())
+    obs = sim.step(1500)
+    obs_o, _ = o.step(1500, want_hashes=False)
+    assert np.array_equal(obs, obs_o)
+    assert engine.state_hash(p, sim.get_state()) == o.hash()
+
+
 def test_chunked_steps_equal_single_steps():
     p = params(seed=3, **DENSE)
     o = O.Oracle(p)

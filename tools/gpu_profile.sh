@@ -24,10 +24,11 @@ run fetch --kernel-trace --pmc FETCH_SIZE --output-format csv
 run write --kernel-trace --pmc WRITE_SIZE --output-format csv
 run sq --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES --output-format csv
 run tcc --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv
+run sq2 --kernel-trace --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv || true
 {
   echo "== kernel trace (mean us per launch)"
   python3 "$root/tools/prof_summary.py" "$(find "$out/trace" -name "*kernel_trace.csv" -print -quit)" 10
-  for p in fetch write sq tcc; do
+  for p in fetch write sq tcc sq2; do
     echo "== $p"
     python3 "$root/tools/pmc_summary.py" $(find "$out/$p" -name '*counter_collection.csv') </dev/null
   done
