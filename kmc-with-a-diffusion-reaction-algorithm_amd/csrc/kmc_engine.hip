@@ -198,9 +198,7 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   rc |= dalloc(s, &d.cell_cnt, s->ncell);
   rc |= dalloc(s, &d.cell_start, s->ncell + 1);
   rc |= dalloc(s, &d.block_sums, s->nscan_blocks);
-  rc |= dalloc(s, &d.rec_pos, (size_t)2 * N);
-  rc |= dalloc(s, &d.rec_id, (size_t)2 * N);
-  rc |= dalloc(s, &d.rec_site, (size_t)2 * N);
+  rc |= dalloc(s, &d.rec, (size_t)2 * N);
   // collision candidates: ~1 per proposal at the benchmark densities; every
   // pair of records for small dense systems
   d.cap_cand = (uint32_t)std::max<uint64_t>(8ull * N, std::min<uint64_t>(4ull * N * N, 1ull << 22));

@@ -47,9 +47,7 @@ struct Dev {
   int32_t* cell_cnt;    // [ncell]
   int32_t* cell_start;  // [ncell+1]
   int32_t* block_sums;  // [scan blocks]
-  float4* rec_pos;      // [2N]
-  int2* rec_id;         // [2N]  {pid | st3<<29 | st2<<30 | isnew<<31, owner key}
-  float2* rec_site;     // [2N]  receptor [3][3] site xy (float)
+  struct Rec* rec;      // [2N] cell-sorted records (old and proposed position of every protein)
   int2* cand;           // [cap_cand] collision candidates (proposal record, other record)
   int2* conf;           // [cap_cand] conflict entries (u, kq | isnew<<31)
   uint32_t cap_cand;
@@ -65,6 +63,13 @@ struct Dev {
   uint32_t* vtag;       // [N]
   Ctl* ctl;
   struct kmc_obs_dev* obs;
+};
+
+// one cell-sorted record (32 B): float reference point, ids, cis site
+struct alignas(16) Rec {
+  float4 pos;   // x, y of bead [1][1]; z span (receptor: lowest/highest domain; ligand: centre)
+  int2 id;      // {pid | st3<<29 | st2<<30 | isnew<<31, owner key}
+  float2 site;  // receptor [3][3] site xy (reaction prefilter); 0 for ligands
 };
 
 struct kmc_obs_dev {  // == kmc_obs
@@ -891,10 +896,12 @@ __global__ void k_rec_scatter(KParams P, Dev d) {
     ref_point(d, w ? d.nxt : d.cur, p, P.NA, x, y, zl, zh);
     int c = cell_y(P, y) * P.ncx + cell_x(P, x);
     int pos = d.cell_start[c] + atomicSub(&d.cell_cnt[c], 1) - 1;  // leaves cell_cnt zeroed
-    d.rec_pos[pos] = make_float4((float)x, (float)y, (float)zl, (float)zh);
-    d.rec_id[pos] = make_int2(p | st | (w << 31), d.owner[p]);
-    const Beads& B = w ? d.nxt : d.cur;  // cis site [3][3] (reaction prefilter)
-    d.rec_site[pos] = p < NA ? make_float2((float)B.A(p, 3, 3, 0), (float)B.A(p, 3, 3, 1)) : make_float2(0.f, 0.f);
+    const Beads& B = w ? d.nxt : d.cur;
+    Rec rc;
+    rc.pos = make_float4((float)x, (float)y, (float)zl, (float)zh);
+    rc.id = make_int2(p | st | (w << 31), d.owner[p]);
+    rc.site = p < NA ? make_float2((float)B.A(p, 3, 3, 0), (float)B.A(p, 3, 3, 1)) : make_float2(0.f, 0.f);
+    d.rec[pos] = rc;  // one 32-byte store
   }
 }
 
@@ -1105,8 +1112,8 @@ __device__ bool tile_load(const KParams& P, const Dev& d, int tx, int ty, TileLd
       int l = min(base + k * (int)blockDim.x + (int)threadIdx.x, n - 1);
       hyk[k] = halo_search(&T.cstart[0][0], HALO + 1, l);
       g[k] = l + T.goff[hyk[k]];
-      p[k] = d.rec_pos[g[k]];
-      id[k] = d.rec_id[g[k]];
+      p[k] = d.rec[g[k]].pos;
+      id[k] = d.rec[g[k]].id;
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -1117,7 +1124,7 @@ __device__ bool tile_load(const KParams& P, const Dev& d, int tx, int ty, TileLd
         T.id[l] = id[k];
         T.cell[l] = (uint16_t)(hyk[k] * HALO + hx);
         if (site) {
-          site[l] = d.rec_site[g[k]];
+          site[l] = d.rec[g[k]].site;
           fin[l] = (id[k].x < 0) == (d.rfinal[id[k].x & RID_PID] != 0);
         }
       }
@@ -1143,9 +1150,21 @@ __device__ __forceinline__ void col_emit(const Dev& d, WgList& L, int rs, int rg
 // pos/ids: record source (LDS or global); rows k=0..2: [r0[k], r1[k]) with
 // global index = r + goff[k].  The three row ranges are walked as one loop and
 // the filters are branch-free (lanes of a wave stay converged).
-__device__ __forceinline__ void col_scan_rec(const KParams& P, const Dev& d, WgList& L, const float4* pos,
-                                             const int2* ids, const int* r0, const int* r1, const int* goff, int rs,
-                                             int2 me, float4 mp) {
+struct LdsRecs {
+  const float4* pos;
+  const int2* ids;
+  __device__ float4 p(int r) const { return pos[r]; }
+  __device__ int2 id(int r) const { return ids[r]; }
+};
+struct GlbRecs {
+  const Rec* rec;
+  __device__ float4 p(int r) const { return rec[r].pos; }
+  __device__ int2 id(int r) const { return rec[r].id; }
+};
+
+template <class S>
+__device__ __forceinline__ void col_scan_rec(const KParams& P, const Dev& d, WgList& L, S src, const int* r0,
+                                             const int* r1, const int* goff, int rs, int2 me, float4 mp) {
   const int NA = P.NA;
   const int m = me.x & RID_PID, u = me.y;
   if (u < 0) {
@@ -1157,8 +1176,8 @@ __device__ __forceinline__ void col_scan_rec(const KParams& P, const Dev& d, WgL
   for (int t = 0; t < tot; ++t) {
     const bool k0 = t < l0, k1 = t < l01;
     const int r = k0 ? r0[0] + t : (k1 ? r0[1] + (t - l0) : r0[2] + (t - l01));
-    const int2 id = ids[r];
-    const float4 rp = pos[r];
+    const int2 id = src.id(r);
+    const float4 rp = src.p(r);
     const int q = id.x & RID_PID, kq = id.y;
     const bool isnew = id.x < 0;
     const bool own_ok = kq == u ? isnew : (kq > u ? !isnew : true);
@@ -1197,7 +1216,7 @@ __global__ void __launch_bounds__(256) k_col_scan(KParams P, Dev d) {
         r1[k] = T.cstart[hy - 1 + k][hx + 2];
         go[k] = T.goff[hy - 1 + k];
       }
-      col_scan_rec(P, d, L, T.pos, T.id, r0, r1, go, l + T.goff[hy], T.id[l], T.pos[l]);
+      col_scan_rec(P, d, L, LdsRecs{T.pos, T.id}, r0, r1, go, l + T.goff[hy], T.id[l], T.pos[l]);
     }
     wg_flush(L, &d.ctl->n_cand, d.cand, d.cap_cand, &d.ctl->err);
     return;
@@ -1217,9 +1236,9 @@ __global__ void __launch_bounds__(256) k_col_scan(KParams P, Dev d) {
     }
     int s0 = d.cell_start[y * P.ncx + x], s1 = d.cell_start[y * P.ncx + x + 1];
     for (int r = s0; r < s1; ++r) {
-      int2 me = d.rec_id[r];
+      int2 me = d.rec[r].id;
       if (me.x >= 0) continue;
-      col_scan_rec(P, d, L, d.rec_pos, d.rec_id, r0, r1, go, r, me, d.rec_pos[r]);
+      col_scan_rec(P, d, L, GlbRecs{d.rec}, r0, r1, go, r, me, d.rec[r].pos);
     }
   }
   wg_flush(L, &d.ctl->n_cand, d.cand, d.cap_cand, &d.ctl->err);
@@ -1237,7 +1256,7 @@ __global__ void k_col_exact(KParams P, Dev d) {
   if (n > d.cap_cand) n = d.cap_cand;
   for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
     int2 c = d.cand[t];
-    int2 a = d.rec_id[c.x], b = d.rec_id[c.y];
+    int2 a = d.rec[c.x].id, b = d.rec[c.y].id;
     int m = a.x & RID_PID, u = a.y, q = b.x & RID_PID, kq = b.y;
     bool isnew = b.x < 0;
     Own o;
@@ -1367,12 +1386,8 @@ __device__ __forceinline__ void rxn_emit(const Dev& d, WgList& L, int i, int q) 
   wg_emit(L, make_int2(i, q), &d.ctl->n_pairs, d.pairs, d.cap_pairs, &d.ctl->err);
 }
 
-// one receptor record; LDS: record r's site/final from site[]/fin[],
-// global: from rec_site / rfinal
-template <bool LDS>
-__device__ __forceinline__ void rxn_scan_rec(const KParams& P, const Dev& d, WgList& L, const float4* pos,
-                                             const int2* ids,
-                                             const float2* site, const uint8_t* fin, const int* r0, const int* r1,
+// one receptor record, records from global memory (dense tiles)
+__device__ __forceinline__ void rxn_scan_glb(const KParams& P, const Dev& d, WgList& L, const int* r0, const int* r1,
                                              int2 me, float4 mp, float2 ms) {
   const int NA = P.NA, NB = P.NB;
   const int i = me.x & RID_PID;
@@ -1381,10 +1396,10 @@ __device__ __forceinline__ void rxn_scan_rec(const KParams& P, const Dev& d, WgL
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     for (int r = r0[k]; r < r1[k]; ++r) {
-      int2 id = ids[r];
+      int2 id = d.rec[r].id;
       int q = id.x & RID_PID;
       if (q == i) continue;
-      float4 rp = pos[r];
+      float4 rp = d.rec[r].pos;
       float dx = rp.x - mp.x, dy = rp.y - mp.y;
       float dxy2 = dx * dx + dy * dy;
       if (q >= NA) {
@@ -1395,12 +1410,11 @@ __device__ __forceinline__ void rxn_scan_rec(const KParams& P, const Dev& d, WgL
         if (!(dxy2 < 57.0f * 57.0f)) continue;
         float gap = fmaxf(fmaxf(rp.z - mp.w, mp.z - rp.w), 0.0f);
         if (!(gap < 16.0f)) continue;
-        float2 qs = LDS ? site[r] : d.rec_site[r];
+        float2 qs = d.rec[r].site;
         float tx = qs.x - ms.x, ty = qs.y - ms.y;
         if (!(tx * tx + ty * ty < 16.0f * 16.0f)) continue;
       }
-      bool f = LDS ? fin[r] != 0 : record_final(d, id);
-      if (!f) continue;
+      if (!record_final(d, id)) continue;
       rxn_emit(d, L, i, q);
     }
   }
@@ -1484,10 +1498,9 @@ __global__ void __launch_bounds__(256) k_rxn_scan_tile(KParams P, Dev d) {
     }
     int s0 = d.cell_start[y * P.ncx + x], s1 = d.cell_start[y * P.ncx + x + 1];
     for (int r = s0; r < s1; ++r) {
-      int2 me = d.rec_id[r];
+      int2 me = d.rec[r].id;
       if ((me.x & RID_PID) >= NA || ((me.x & RID_ST2) && (me.x & RID_ST3)) || !record_final(d, me)) continue;
-      rxn_scan_rec<false>(P, d, L, d.rec_pos, d.rec_id, nullptr, nullptr, r0, r1, me, d.rec_pos[r],
-                          d.rec_site[r]);
+      rxn_scan_glb(P, d, L, r0, r1, me, d.rec[r].pos, d.rec[r].site);
     }
   }
   wg_flush(L, &d.ctl->n_pairs, d.pairs, d.cap_pairs, &d.ctl->err);
