@@ -29,6 +29,7 @@ struct KParams {
   double T_aa, T_ab, T_bb, T_bond, T_cis;
   kmcr::Key key;
   int tcap;  // LDS tile record capacity (<= TCAP; lowered only to test the global path)
+  int tile;  // cells per tile side of the LDS scans (<= TILE_MAX)
 };
 
 // per-step control block in device memory (replayable without host writes)

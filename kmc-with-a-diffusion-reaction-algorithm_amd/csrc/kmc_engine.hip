@@ -228,6 +228,16 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   const char* tc = getenv("KMC_DEBUG_TCAP");
   K.tcap = TCAP;
   if (tc && *tc) K.tcap = std::max(0, std::min(TCAP, atoi(tc)));
+  // tile side of the LDS scans: about 200 proposal records per 256-thread
+  // workgroup, halo records well inside TCAP (mean density of the box)
+  {
+    const double rho = (double)N * K.cs * K.cs / std::max(1.0, p->box_x * p->box_y);  // proteins per cell
+    int t = TILE_MAX;
+    while (t > 4 && (t * t * rho > 205.0 || (t + 2) * (t + 2) * 2.0 * rho > 0.6 * TCAP)) --t;
+    const char* te = getenv("KMC_TILE");
+    if (te && *te) t = std::max(2, std::min(TILE_MAX, atoi(te)));
+    K.tile = t;
+  }
   *out = s;
   return KMC_OK;
 }
@@ -395,7 +405,7 @@ static int launch_step(kmc_sim* s) {
   });
   TIMED(KI_REC_SCATTER, (k_rec_scatter<<<gN, T, 0, st>>>(K, d)));
   const int gX = std::min(2048, (K.N + T - 1) / T);  // grid-stride kernels over device-sized lists
-  const int ntiles = ((K.ncx + TILE - 1) / TILE) * ((K.ncy + TILE - 1) / TILE);
+  const int ntiles = ((K.ncx + K.tile - 1) / K.tile) * ((K.ncy + K.tile - 1) / K.tile);
   TIMED(KI_COL_SCAN, (k_col_scan<<<ntiles, 256, 0, st>>>(K, d)));
   TIMED(KI_COL_EXACT, (k_col_exact<<<gX, T, 0, st>>>(K, d)));
   TIMED(KI_COL_ROUNDS, {

@@ -1039,39 +1039,45 @@ __device__ __forceinline__ void wg_flush(WgList& L, uint32_t* gctr, int2* gout, 
 }
 
 // ---------------------------------------------------------------- LDS tiles
-// A workgroup owns a TILE×TILE block of cells.  It stages the records of the
-// block plus a one-cell halo into LDS (a halo row of cells is one contiguous
-// range of the cell-sorted record array; all loads are issued up front), then
-// each thread takes interior records and scans their 3x3 cells from LDS.
-#define TILE 16
-#define HALO (TILE + 2)
-#define TCAP 1280
+// A workgroup owns a tile×tile block of cells (tile chosen on the host from
+// the record density so that a block holds about 200 scanning records for
+// its 256 threads).  It stages the records of the block plus a one-cell halo
+// into LDS (a halo row of cells is one contiguous range of the cell-sorted
+// array; all loads are issued up front), lists the block's scanning records
+// as work items, and each thread scans one item's 3x3 cells from LDS.
+#define TILE_MAX 16
+#define HALO_MAX (TILE_MAX + 2)
+#define TCAP 1024
+#define RID_FIN (1 << 24)  // staged record is its protein's final position (reaction scan)
 struct TileLds {
   float4 pos[TCAP];
   int2 id[TCAP];
-  uint16_t cell[TCAP];         // hy * HALO + hx of each staged record
-  int cstart[HALO][HALO + 1];  // LDS index of each halo cell's first record; [hy][HALO] = row end
-  int goff[HALO];              // global record index − LDS index, per halo row
+  uint32_t item[TCAP];                 // work item: LDS record index | halo cell << 16
+  int cstart[HALO_MAX][HALO_MAX + 1];  // LDS index of each halo cell's first record; [hy][halo] = row end
+  int goff[HALO_MAX];                  // global record index − LDS index, per halo row
   int n;
+  uint32_t nitem;
 };
 
-// largest i in [0, HALO) with a[i] <= v  (a non-decreasing, a[0] <= v)
-__device__ __forceinline__ int halo_search(const int* a, int stride, int v) {
+// largest i in [0, cnt) with a[i * stride] <= v  (non-decreasing, a[0] <= v, cnt <= 32)
+__device__ __forceinline__ int halo_search(const int* a, int stride, int v, int cnt) {
   int i = 0;
 #pragma unroll
   for (int s = 16; s; s >>= 1)
-    if (i + s < HALO && a[(i + s) * stride] <= v) i += s;
+    if (i + s < cnt && a[(i + s) * stride] <= v) i += s;
   return i;
 }
 
 // Returns false (uniformly) when the tile holds more than P.tcap records; the
-// caller then takes the global-memory path.  site/fin (reaction scan only):
-// the [3][3] site of each record and whether it is the protein's final position.
-__device__ bool tile_load(const KParams& P, const Dev& d, int tx, int ty, TileLds& T, float2* site, uint8_t* fin) {
-  const int cx0 = tx * TILE - 1, cy0 = ty * TILE - 1;
-  const int xlo = max(cx0, 0), xhi = min(cx0 + HALO - 1, P.ncx - 1);
-  for (int idx = threadIdx.x; idx < HALO * (HALO + 1); idx += blockDim.x) {
-    int hy = idx / (HALO + 1), hx = idx % (HALO + 1);
+// caller then takes the global-memory path.  site (reaction scan only): the
+// [3][3] site of each record; its final flag goes into id.x as RID_FIN.
+__device__ bool tile_load(const KParams& P, const Dev& d, int tx, int ty, TileLds& T, float2* site) {
+  const int tile = P.tile, halo = tile + 2;
+  const int cx0 = tx * tile - 1, cy0 = ty * tile - 1;
+  const int xlo = max(cx0, 0), xhi = min(cx0 + halo - 1, P.ncx - 1);
+  if (threadIdx.x == 0) T.nitem = 0;
+  for (int idx = threadIdx.x; idx < halo * (halo + 1); idx += blockDim.x) {
+    int hy = idx / (halo + 1), hx = idx - hy * (halo + 1);
     int y = cy0 + hy;
     int v = 0;
     if (y >= 0 && y < P.ncy && xlo <= xhi) {
@@ -1083,19 +1089,19 @@ __device__ bool tile_load(const KParams& P, const Dev& d, int tx, int ty, TileLd
   __syncthreads();
   if (threadIdx.x < 64) {  // row lengths -> LDS row bases (wave-0 inclusive scan)
     int hy = threadIdx.x;
-    int len = hy < HALO ? T.cstart[hy][HALO] - T.cstart[hy][0] : 0;
+    int len = hy < halo ? T.cstart[hy][halo] - T.cstart[hy][0] : 0;
     int inc = len;
 #pragma unroll
     for (int o = 1; o < 32; o <<= 1) {
       int t = __shfl_up(inc, o, 64);
       if (hy >= o) inc += t;
     }
-    if (hy < HALO) T.goff[hy] = T.cstart[hy][0] - (inc - len);
-    if (hy == HALO - 1) T.n = inc;
+    if (hy < halo) T.goff[hy] = T.cstart[hy][0] - (inc - len);
+    if (hy == halo - 1) T.n = inc;
   }
   __syncthreads();
-  for (int idx = threadIdx.x; idx < HALO * (HALO + 1); idx += blockDim.x) {
-    int hy = idx / (HALO + 1), hx = idx % (HALO + 1);
+  for (int idx = threadIdx.x; idx < halo * (halo + 1); idx += blockDim.x) {
+    int hy = idx / (halo + 1), hx = idx - hy * (halo + 1);
     T.cstart[hy][hx] -= T.goff[hy];
   }
   __syncthreads();
@@ -1104,34 +1110,67 @@ __device__ bool tile_load(const KParams& P, const Dev& d, int tx, int ty, TileLd
   // four records per thread in flight: loads from clamped indices first, then
   // the LDS stores (keeps the staging arrays in registers)
   for (int base = 0; base < n; base += 4 * blockDim.x) {
-    float4 p[4];
-    int2 id[4];
-    int hyk[4], g[4];
+    Rec rc[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       int l = min(base + k * (int)blockDim.x + (int)threadIdx.x, n - 1);
-      hyk[k] = halo_search(&T.cstart[0][0], HALO + 1, l);
-      g[k] = l + T.goff[hyk[k]];
-      p[k] = d.rec[g[k]].pos;
-      id[k] = d.rec[g[k]].id;
+      int hy = halo_search(&T.cstart[0][0], HALO_MAX + 1, l, halo);
+      rc[k] = d.rec[l + T.goff[hy]];
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       int l = base + k * (int)blockDim.x + (int)threadIdx.x;
       if (l < n) {
-        int hx = halo_search(&T.cstart[hyk[k]][0], 1, l);
-        T.pos[l] = p[k];
-        T.id[l] = id[k];
-        T.cell[l] = (uint16_t)(hyk[k] * HALO + hx);
+        int2 id = rc[k].id;
         if (site) {
-          site[l] = d.rec[g[k]].site;
-          fin[l] = (id[k].x < 0) == (d.rfinal[id[k].x & RID_PID] != 0);
+          site[l] = rc[k].site;
+          if ((id.x < 0) == (d.rfinal[id.x & RID_PID] != 0)) id.x |= RID_FIN;
         }
+        T.pos[l] = rc[k].pos;
+        T.id[l] = id;
       }
     }
   }
   __syncthreads();
   return true;
+}
+
+// The block's interior records satisfying pred(id) become work items (all
+// threads call; ends with a barrier).
+template <class Pred>
+__device__ __forceinline__ void tile_items(const KParams& P, TileLds& T, Pred pred) {
+  const int tile = P.tile, halo = tile + 2;
+  for (int l = threadIdx.x; l < T.n; l += blockDim.x) {
+    int hy = halo_search(&T.cstart[0][0], HALO_MAX + 1, l, halo);
+    if (hy < 1 || hy > tile || l < T.cstart[hy][1] || l >= T.cstart[hy][tile + 1]) continue;
+    if (!pred(T.id[l])) continue;
+    int hx = halo_search(&T.cstart[hy][0], 1, l, halo);
+    T.item[wave_slot(&T.nitem)] = (uint32_t)l | (uint32_t)(hy * HALO_MAX + hx) << 16;
+  }
+  __syncthreads();
+}
+
+// the 3x3 record ranges of work item c (halo cell hy * HALO_MAX + hx)
+__device__ __forceinline__ void item_ranges(const TileLds& T, int c, int* r0, int* r1, int* go) {
+  const int hy = c / HALO_MAX, hx = c - hy * HALO_MAX;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    r0[k] = T.cstart[hy - 1 + k][hx - 1];
+    r1[k] = T.cstart[hy - 1 + k][hx + 2];
+    if (go) go[k] = T.goff[hy - 1 + k];
+  }
+}
+
+// global-memory path (dense tile): the 3x3 record ranges of cell (x, y)
+__device__ __forceinline__ void cell_ranges(const KParams& P, const Dev& d, int x, int y, int* r0, int* r1) {
+  int x0 = max(x - 1, 0), x1 = min(x + 1, P.ncx - 1);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    int yy = y - 1 + k;
+    bool ok = yy >= 0 && yy < P.ncy;
+    r0[k] = ok ? d.cell_start[yy * P.ncx + x0] : 0;
+    r1[k] = ok ? d.cell_start[yy * P.ncx + x1 + 1] : 0;
+  }
 }
 
 // ---------------------------------------------------------------- 4a. scan
@@ -1147,9 +1186,6 @@ __device__ __forceinline__ void col_emit(const Dev& d, WgList& L, int rs, int rg
   wg_emit(L, make_int2(rs, rg), &d.ctl->n_cand, d.cand, d.cap_cand, &d.ctl->err);
 }
 
-// pos/ids: record source (LDS or global); rows k=0..2: [r0[k], r1[k]) with
-// global index = r + goff[k].  The three row ranges are walked as one loop and
-// the filters are branch-free (lanes of a wave stay converged).
 struct LdsRecs {
   const float4* pos;
   const int2* ids;
@@ -1162,6 +1198,9 @@ struct GlbRecs {
   __device__ int2 id(int r) const { return rec[r].id; }
 };
 
+// src: record source (LDS or global); rows k=0..2: [r0[k], r1[k]) with
+// global index = r + goff[k].  The three row ranges are walked as one loop and
+// the filters are branch-free (lanes of a wave stay converged).
 template <class S>
 __device__ __forceinline__ void col_scan_rec(const KParams& P, const Dev& d, WgList& L, S src, const int* r0,
                                              const int* r1, const int* goff, int rs, int2 me, float4 mp) {
@@ -1191,49 +1230,29 @@ __device__ __forceinline__ void col_scan_rec(const KParams& P, const Dev& d, WgL
 __global__ void __launch_bounds__(256) k_col_scan(KParams P, Dev d) {
   __shared__ TileLds T;
   __shared__ WgList L;
-  __shared__ uint16_t work[TCAP];  // the tile's interior proposal records
-  __shared__ uint32_t nwork;
-  const int ntx = (P.ncx + TILE - 1) / TILE;
+  const int ntx = (P.ncx + P.tile - 1) / P.tile;
   const int tx = blockIdx.x % ntx, ty = blockIdx.x / ntx;
-  if (threadIdx.x == 0) nwork = 0;
   wg_list_init(L);
-  if (tile_load(P, d, tx, ty, T, nullptr, nullptr)) {
-    for (int l = threadIdx.x; l < T.n; l += blockDim.x) {
-      int c = T.cell[l];
-      int hy = c / HALO, hx = c - hy * HALO;
-      if (hx >= 1 && hx <= TILE && hy >= 1 && hy <= TILE && T.id[l].x < 0) work[wave_slot(&nwork)] = (uint16_t)l;
-    }
-    __syncthreads();
-    const int nw = nwork;
-    for (int w = threadIdx.x; w < nw; w += blockDim.x) {
-      const int l = work[w];
-      const int c = T.cell[l];
-      const int hy = c / HALO, hx = c - hy * HALO;
+  if (tile_load(P, d, tx, ty, T, nullptr)) {
+    tile_items(P, T, [](int2 id) { return id.x < 0; });  // proposal records
+    const int ni = T.nitem;
+    for (int w = threadIdx.x; w < ni; w += blockDim.x) {
+      const uint32_t it = T.item[w];
+      const int l = it & 0xffff;
       int r0[3], r1[3], go[3];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        r0[k] = T.cstart[hy - 1 + k][hx - 1];
-        r1[k] = T.cstart[hy - 1 + k][hx + 2];
-        go[k] = T.goff[hy - 1 + k];
-      }
+      item_ranges(T, it >> 16, r0, r1, go);
+      const int hy = (it >> 16) / HALO_MAX;
       col_scan_rec(P, d, L, LdsRecs{T.pos, T.id}, r0, r1, go, l + T.goff[hy], T.id[l], T.pos[l]);
     }
     wg_flush(L, &d.ctl->n_cand, d.cand, d.cap_cand, &d.ctl->err);
     return;
   }
   // dense tile: one thread per interior cell, records from global memory
-  for (int c = threadIdx.x; c < TILE * TILE; c += blockDim.x) {
-    int x = tx * TILE + c % TILE, y = ty * TILE + c / TILE;
+  for (int c = threadIdx.x; c < P.tile * P.tile; c += blockDim.x) {
+    int x = tx * P.tile + c % P.tile, y = ty * P.tile + c / P.tile;
     if (x >= P.ncx || y >= P.ncy) continue;
     int r0[3], r1[3], go[3] = {0, 0, 0};
-    int x0 = max(x - 1, 0), x1 = min(x + 1, P.ncx - 1);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      int yy = y - 1 + k;
-      bool ok = yy >= 0 && yy < P.ncy;
-      r0[k] = ok ? d.cell_start[yy * P.ncx + x0] : 0;
-      r1[k] = ok ? d.cell_start[yy * P.ncx + x1 + 1] : 0;
-    }
+    cell_ranges(P, d, x, y, r0, r1);
     int s0 = d.cell_start[y * P.ncx + x], s1 = d.cell_start[y * P.ncx + x + 1];
     for (int r = s0; r < s1; ++r) {
       int2 me = d.rec[r].id;
@@ -1421,8 +1440,8 @@ __device__ __forceinline__ void rxn_scan_glb(const KParams& P, const Dev& d, WgL
 }
 
 __device__ __forceinline__ void rxn_scan_lds(const KParams& P, const Dev& d, WgList& L, const TileLds& T,
-                                             const float2* site, const uint8_t* fin, const int* r0, const int* r1,
-                                             int2 me, float4 mp, float2 ms) {
+                                             const float2* site, const int* r0, const int* r1, int2 me, float4 mp,
+                                             float2 ms) {
   const int NA = P.NA, NB = P.NB;
   const int i = me.x & RID_PID;
   const bool want_rl = !(me.x & RID_ST2) && NB > 0;
@@ -1442,60 +1461,39 @@ __device__ __forceinline__ void rxn_scan_lds(const KParams& P, const Dev& d, WgL
     const float tx = qs.x - ms.x, ty = qs.y - ms.y;
     const bool cis_ok = !isB & want_cis & !(id.x & RID_ST3) & (dxy2 < 57.0f * 57.0f) & (gap < 16.0f) &
                         (tx * tx + ty * ty < 16.0f * 16.0f);
-    if ((q != i) & (rl_ok | cis_ok) & (fin[r] != 0)) rxn_emit(d, L, i, q);
+    if ((q != i) & (rl_ok | cis_ok) & ((id.x & RID_FIN) != 0)) rxn_emit(d, L, i, q);
   }
 }
 
 __global__ void __launch_bounds__(256) k_rxn_scan_tile(KParams P, Dev d) {
   __shared__ TileLds T;
   __shared__ float2 site[TCAP];
-  __shared__ uint8_t fin[TCAP];
   __shared__ WgList L;
-  __shared__ uint16_t work[TCAP];  // the tile's interior final receptor records that can react
-  __shared__ uint32_t nwork;
-  const int ntx = (P.ncx + TILE - 1) / TILE;
+  const int ntx = (P.ncx + P.tile - 1) / P.tile;
   const int tx = blockIdx.x % ntx, ty = blockIdx.x / ntx;
   const int NA = P.NA;
-  if (threadIdx.x == 0) nwork = 0;
   wg_list_init(L);
-  if (tile_load(P, d, tx, ty, T, site, fin)) {
-    for (int l = threadIdx.x; l < T.n; l += blockDim.x) {
-      int c = T.cell[l];
-      int hy = c / HALO, hx = c - hy * HALO;
-      int2 me = T.id[l];
-      if (hx >= 1 && hx <= TILE && hy >= 1 && hy <= TILE && (me.x & RID_PID) < NA &&
-          !((me.x & RID_ST2) && (me.x & RID_ST3)) && fin[l])
-        work[wave_slot(&nwork)] = (uint16_t)l;
-    }
-    __syncthreads();
-    const int nw = nwork;
-    for (int w = threadIdx.x; w < nw; w += blockDim.x) {
-      const int l = work[w];
-      const int c = T.cell[l];
-      const int hy = c / HALO, hx = c - hy * HALO;
+  if (tile_load(P, d, tx, ty, T, site)) {
+    // final receptor records that can still react
+    tile_items(P, T, [NA](int2 id) {
+      return (id.x & RID_PID) < NA && !((id.x & RID_ST2) && (id.x & RID_ST3)) && (id.x & RID_FIN);
+    });
+    const int ni = T.nitem;
+    for (int w = threadIdx.x; w < ni; w += blockDim.x) {
+      const uint32_t it = T.item[w];
+      const int l = it & 0xffff;
       int r0[3], r1[3];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        r0[k] = T.cstart[hy - 1 + k][hx - 1];
-        r1[k] = T.cstart[hy - 1 + k][hx + 2];
-      }
-      rxn_scan_lds(P, d, L, T, site, fin, r0, r1, T.id[l], T.pos[l], site[l]);
+      item_ranges(T, it >> 16, r0, r1, nullptr);
+      rxn_scan_lds(P, d, L, T, site, r0, r1, T.id[l], T.pos[l], site[l]);
     }
     wg_flush(L, &d.ctl->n_pairs, d.pairs, d.cap_pairs, &d.ctl->err);
     return;
   }
-  for (int c = threadIdx.x; c < TILE * TILE; c += blockDim.x) {
-    int x = tx * TILE + c % TILE, y = ty * TILE + c / TILE;
+  for (int c = threadIdx.x; c < P.tile * P.tile; c += blockDim.x) {
+    int x = tx * P.tile + c % P.tile, y = ty * P.tile + c / P.tile;
     if (x >= P.ncx || y >= P.ncy) continue;
     int r0[3], r1[3];
-    int x0 = max(x - 1, 0), x1 = min(x + 1, P.ncx - 1);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      int yy = y - 1 + k;
-      bool ok = yy >= 0 && yy < P.ncy;
-      r0[k] = ok ? d.cell_start[yy * P.ncx + x0] : 0;
-      r1[k] = ok ? d.cell_start[yy * P.ncx + x1 + 1] : 0;
-    }
+    cell_ranges(P, d, x, y, r0, r1);
     int s0 = d.cell_start[y * P.ncx + x], s1 = d.cell_start[y * P.ncx + x + 1];
     for (int r = s0; r < s1; ++r) {
       int2 me = d.rec[r].id;
