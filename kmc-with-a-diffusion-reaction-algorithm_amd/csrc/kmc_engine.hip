@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <hipcub/hipcub.hpp>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -20,12 +21,12 @@ using namespace kmcd;
 enum KId {
   KI_CLASSIFY, KI_BFS, KI_BFS_OVF, KI_PROPOSE, KI_COMPLEX, KI_REC_COUNT, KI_SCAN, KI_REC_SCATTER,
   KI_COL_SCAN, KI_COL_EXACT, KI_COL_ROUNDS, KI_COMMIT, KI_RXN_SCAN, KI_RXN_EXACT, KI_RL_MATCH, KI_CIS_MATCH, KI_DISS_RL,
-  KI_DISS_CIS, KI_OBSERVE, KI_FINALIZE, KI_N
+  KI_DISS_CIS, KI_OBSERVE, KI_FINALIZE, KI_RESORT, KI_N
 };
 static const char* const KNAMES[KI_N] = {
     "k_classify", "k_bfs", "k_bfs_overflow", "k_propose", "k_complex", "k_rec_count", "k_scan",
     "k_rec_scatter", "k_col_scan", "k_col_exact", "k_col_rounds", "k_commit", "k_rxn_scan", "k_rxn_exact",
-    "k_rl_match", "k_cis_match", "k_diss_rl", "k_diss_cis", "k_observe", "k_finalize"};
+    "k_rl_match", "k_cis_match", "k_diss_rl", "k_diss_cis", "k_observe", "k_finalize", "slot_resort"};
 #define TRING 64  // steps of event pairs kept in flight
 
 struct kmc_sim {
@@ -43,6 +44,14 @@ struct kmc_sim {
   int64_t obs_cap = 0;
   Ctl* ctl_host = nullptr;
   bool poison = false;
+  // slot order (kmc_kernels.hip §slot order): scratch of the re-sort
+  int64_t resort_every = 100, since_resort = 0;
+  int key_bits = 1;
+  uint32_t *skeys = nullptr, *skeys2 = nullptr;
+  int32_t *svals = nullptr, *svals2 = nullptr, *perm = nullptr, *newslot = nullptr;
+  int32_t *a_tmp = nullptr, *b_tmp = nullptr, *id_tmp = nullptr;
+  void* sort_tmp = nullptr;
+  size_t sort_tmp_bytes = 0;
   // per-kernel timing: a ring of TRING steps of event pairs, read back lazily
   uint64_t tmask = 0;
   std::vector<hipEvent_t> tev;  // [TRING][KI_N][2]
@@ -185,6 +194,17 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   rc |= dalloc(s, &d.a_int, (size_t)5 * NA);
   rc |= dalloc(s, &d.b_int, (size_t)8 * NB);
   rc |= dalloc(s, &d.owner, N);
+  rc |= dalloc(s, &d.id_of, N);
+  rc |= dalloc(s, &d.slot_of, N);
+  rc |= dalloc(s, &s->id_tmp, N);
+  rc |= dalloc(s, &s->a_tmp, (size_t)5 * NA);
+  rc |= dalloc(s, &s->b_tmp, (size_t)8 * NB);
+  rc |= dalloc(s, &s->skeys, N);
+  rc |= dalloc(s, &s->skeys2, N);
+  rc |= dalloc(s, &s->svals, N);
+  rc |= dalloc(s, &s->svals2, N);
+  rc |= dalloc(s, &s->perm, N);
+  rc |= dalloc(s, &s->newslot, N);
   rc |= dalloc(s, &d.ukind, N);
   rc |= dalloc(s, &d.ustate, N);
   rc |= dalloc(s, &d.moved, N);
@@ -238,6 +258,26 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
     if (te && *te) t = std::max(2, std::min(TILE_MAX, atoi(te)));
     K.tile = t;
   }
+  {
+    const uint64_t ntx = (K.ncx + K.tile - 1) / K.tile, nty = (K.ncy + K.tile - 1) / K.tile;
+    const uint64_t kmax = ntx * nty * (uint64_t)K.tile * K.tile;
+    s->key_bits = 1;
+    while ((1ull << s->key_bits) < kmax) ++s->key_bits;
+    const char* re = getenv("KMC_RESORT");
+    if (re && *re) s->resort_every = atoll(re);
+    size_t tb = 0;
+    int nmax = std::max(NA, NB);
+    if (hipcub::DeviceRadixSort::SortPairs(nullptr, tb, s->skeys, s->skeys2, s->svals, s->svals2, nmax, 0,
+                                           s->key_bits, s->stream) != hipSuccess) {
+      kmc_destroy(s);
+      return KMC_ERR_HIP;
+    }
+    s->sort_tmp_bytes = std::max<size_t>(tb, 16);
+    if (dalloc(s, (uint8_t**)&s->sort_tmp, s->sort_tmp_bytes) != KMC_OK) {
+      kmc_destroy(s);
+      return KMC_ERR_HIP;
+    }
+  }
   *out = s;
   return KMC_OK;
 }
@@ -256,6 +296,57 @@ int kmc_destroy(kmc_sim* s) {
 }
 
 int64_t kmc_current_step(const kmc_sim* s) { return s ? s->step_done : -1; }
+
+// Gather R, the state rows and bond fields through perm (new index -> old
+// slot) into R_new / scratch, renumbering bond fields through map, and swap.
+static void reorder(kmc_sim* s, const int32_t* perm, const int32_t* map, bool swap_in) {
+  const KParams& K = s->K;
+  Dev& d = s->d;
+  hipStream_t st = s->stream;
+  const int NA = K.NA, NB = K.NB, T = 256;
+  auto g = [&](size_t n) { return (unsigned)((n + T - 1) / T); };
+  if (NA > 0) {
+    k_gather_f64<<<g((size_t)48 * NA), T, 0, st>>>(d.cur.a, d.nxt.a, perm, 0, NA, 48);
+    // a rows: st2 st3 nei2 nei4 nei3 (nei2, nei3 are protein links)
+    k_gather_i32<<<g((size_t)5 * NA), T, 0, st>>>(d.a_int, s->a_tmp, perm, 0, NA, 5, (1u << 2) | (1u << 4), map);
+  }
+  if (NB > 0) {
+    k_gather_f64<<<g((size_t)24 * NB), T, 0, st>>>(d.cur.b, d.nxt.b, perm, NA, NB, 24);
+    k_gather_i32<<<g((size_t)8 * NB), T, 0, st>>>(d.b_int, s->b_tmp, perm, NA, NB, 8, 0xf0u, map);
+  }
+  if (!swap_in) return;
+  std::swap(d.cur.a, d.nxt.a);
+  std::swap(d.cur.b, d.nxt.b);
+  std::swap(d.a_int, s->a_tmp);
+  std::swap(d.b_int, s->b_tmp);
+}
+
+__global__ void k_iota(int32_t* a, int32_t* b, int n) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) a[i] = b[i] = i;
+}
+
+// Re-sort the slots spatially (between steps; R_new is free scratch then).
+static int resort(kmc_sim* s) {
+  const KParams& K = s->K;
+  Dev& d = s->d;
+  hipStream_t st = s->stream;
+  const int NA = K.NA, NB = K.NB, N = K.N, T = 256;
+  k_slot_keys<<<(N + T - 1) / T, T, 0, st>>>(K, d, s->skeys, s->svals);
+  size_t tb = s->sort_tmp_bytes;
+  if (NA > 0)
+    HIPCHK(s, hipcub::DeviceRadixSort::SortPairs(s->sort_tmp, tb, s->skeys, s->skeys2, s->svals, s->svals2, NA, 0,
+                                                 s->key_bits, st));
+  tb = s->sort_tmp_bytes;
+  if (NB > 0)
+    HIPCHK(s, hipcub::DeviceRadixSort::SortPairs(s->sort_tmp, tb, s->skeys + NA, s->skeys2 + NA, s->svals + NA,
+                                                 s->svals2 + NA, NB, 0, s->key_bits, st));
+  k_slot_inverse<<<(N + T - 1) / T, T, 0, st>>>(K, s->svals2, s->perm, s->newslot);
+  reorder(s, s->perm, s->newslot, true);
+  k_gather_ids<<<(N + T - 1) / T, T, 0, st>>>(K, d.id_of, s->id_tmp, d.slot_of, s->perm);
+  std::swap(d.id_of, s->id_tmp);
+  return hipGetLastError() == hipSuccess ? KMC_OK : fail(s, KMC_ERR_HIP, "resort launch");
+}
 
 int kmc_set_state(kmc_sim* s, const kmc_state_view* v) {
   if (!s || !v) return KMC_ERR_ARG;
@@ -282,7 +373,13 @@ int kmc_set_state(kmc_sim* s, const kmc_state_view* v) {
   HIPCHK(s, hipMemcpy(d.ctl, &c, sizeof c, hipMemcpyHostToDevice));
   HIPCHK(s, hipMemset(d.ustate, 0, sizeof(uint32_t) * (size_t)(NA + NB)));
   HIPCHK(s, hipMemset(d.moved, 0, sizeof(uint32_t) * (size_t)(NA + NB)));
+  // reference order = identity slots, then the spatial sort
+  k_iota<<<(NA + NB + 255) / 256, 256, 0, s->stream>>>(d.id_of, d.slot_of, NA + NB);
+  rc = resort(s);
+  if (rc != KMC_OK) return rc;
+  HIPCHK(s, hipStreamSynchronize(s->stream));
   s->step_done = v->step;
+  s->since_resort = 0;
   s->have_state = true;
   return KMC_OK;
 }
@@ -292,11 +389,13 @@ int kmc_get_state(kmc_sim* s, kmc_state_view* v) {
   if (!s->have_state) return fail(s, KMC_ERR_ARG, "no state");
   const int NA = s->p.n_a, NB = s->p.n_b;
   Dev& d = s->d;
+  // slots -> reference order (into R_new / scratch; links renumbered to reference indices)
+  reorder(s, d.slot_of, d.id_of, false);
   HIPCHK(s, hipStreamSynchronize(s->stream));
-  HIPCHK(s, hipMemcpy(v->ra, d.cur.a, sizeof(double) * 48 * (size_t)NA, hipMemcpyDeviceToHost));
-  HIPCHK(s, hipMemcpy(v->rb, d.cur.b, sizeof(double) * 24 * (size_t)NB, hipMemcpyDeviceToHost));
-  HIPCHK(s, hipMemcpy(v->a_int, d.a_int, sizeof(int32_t) * 5 * (size_t)NA, hipMemcpyDeviceToHost));
-  HIPCHK(s, hipMemcpy(v->b_int, d.b_int, sizeof(int32_t) * 8 * (size_t)NB, hipMemcpyDeviceToHost));
+  HIPCHK(s, hipMemcpy(v->ra, d.nxt.a, sizeof(double) * 48 * (size_t)NA, hipMemcpyDeviceToHost));
+  HIPCHK(s, hipMemcpy(v->rb, d.nxt.b, sizeof(double) * 24 * (size_t)NB, hipMemcpyDeviceToHost));
+  HIPCHK(s, hipMemcpy(v->a_int, s->a_tmp, sizeof(int32_t) * 5 * (size_t)NA, hipMemcpyDeviceToHost));
+  HIPCHK(s, hipMemcpy(v->b_int, s->b_tmp, sizeof(int32_t) * 8 * (size_t)NB, hipMemcpyDeviceToHost));
   Ctl c;
   HIPCHK(s, hipMemcpy(&c, d.ctl, sizeof c, hipMemcpyDeviceToHost));
   int rl, mono, cis;
@@ -378,13 +477,18 @@ struct Bracket {
     __VA_ARGS__;      \
   } while (0)
 
-static int launch_step(kmc_sim* s) {
+static int launch_step(kmc_sim* s, bool re_sort) {
   const KParams& K = s->K;
   Dev& d = s->d;
   hipStream_t st = s->stream;
   const int T = 256;
   const int gN = (K.N + T - 1) / T, gA = (K.NA + T - 1) / T, gB = (K.NB + T - 1) / T;
   if (s->tmask) harvest(s, s->tslot);  // the slot's previous use is TRING steps old
+  if (re_sort) {
+    int rc;
+    TIMED(KI_RESORT, rc = resort(s));
+    if (rc != KMC_OK) return rc;
+  }
   if (s->poison) {
     // debug: every bead of R_new must be rewritten by a proposal or a revert
     (void)hipMemsetAsync(d.nxt.a, 0xff, sizeof(double) * 48 * (size_t)K.NA, st);
@@ -449,10 +553,13 @@ int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out) {
     uint32_t zero = 0;
     HIPCHK(s, hipMemcpyAsync(&s->d.ctl->obs_idx, &zero, sizeof zero, hipMemcpyHostToDevice, s->stream));
     for (int64_t k = 0; k < n; ++k) {
+      const bool rs = s->resort_every > 0 && ++s->since_resort >= s->resort_every;
+      if (rs) s->since_resort = 0;
       // unit-state tags are (step mod 2^30): clear them when the tag wraps
       if (((s->step_done + k + 1) & 0x3fffffff) == 0)
         HIPCHK(s, hipMemsetAsync(s->d.ustate, 0, sizeof(uint32_t) * (size_t)s->K.N, s->stream));
-      launch_step(s);
+      int rc = launch_step(s, rs);
+      if (rc != KMC_OK) return rc;
     }
     HIPCHK(s, hipGetLastError());
     HIPCHK(s, hipMemcpyAsync(s->ctl_host, s->d.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, s->stream));
@@ -517,21 +624,26 @@ int kmc_get_clusters(kmc_sim* s, int32_t* row_len, int32_t* members) {
   if (s->step_done == 0 || !s->have_state) return fail(s, KMC_ERR_ARG, "no step simulated yet");
   const int NA = s->p.n_a, NB = s->p.n_b, N = NA + NB;
   std::vector<uint8_t> kind(N);
-  std::vector<int32_t> off(NB), size(NB), mem(N);
+  std::vector<int32_t> off(NB), size(NB), mem(N), id_of(N), slot_of(N);
   HIPCHK(s, hipStreamSynchronize(s->stream));
   HIPCHK(s, hipMemcpy(kind.data(), s->d.ukind, N, hipMemcpyDeviceToHost));
   HIPCHK(s, hipMemcpy(off.data(), s->d.cx_off, sizeof(int32_t) * NB, hipMemcpyDeviceToHost));
   HIPCHK(s, hipMemcpy(size.data(), s->d.cx_size, sizeof(int32_t) * NB, hipMemcpyDeviceToHost));
   HIPCHK(s, hipMemcpy(mem.data(), s->d.members, sizeof(int32_t) * N, hipMemcpyDeviceToHost));
+  HIPCHK(s, hipMemcpy(id_of.data(), s->d.id_of, sizeof(int32_t) * N, hipMemcpyDeviceToHost));
+  HIPCHK(s, hipMemcpy(slot_of.data(), s->d.slot_of, sizeof(int32_t) * N, hipMemcpyDeviceToHost));
+  // unit tables of the last step's classification (slots are re-sorted only
+  // right before a step, so they still use the current slot numbering)
   int64_t o = 0;
   for (int b = 0; b < NB; ++b) {
-    int p = NA + b;
+    int p = slot_of[NA + b];  // ligand b's slot
     if (kind[p] == U_FREE_B) {
       row_len[b] = 1;
-      members[o++] = p + 1;
+      members[o++] = NA + b + 1;
     } else if (kind[p] == U_COMPLEX) {
-      row_len[b] = size[b];
-      for (int t = 0; t < size[b]; ++t) members[o++] = mem[off[b] + t] + 1;
+      int lb = p - NA;
+      row_len[b] = size[lb];
+      for (int t = 0; t < size[lb]; ++t) members[o++] = id_of[mem[off[lb] + t]] + 1;
     } else {
       row_len[b] = 0;
     }

@@ -33,7 +33,9 @@ struct Dev {
   Beads cur, nxt;
   int32_t* a_int;  // [5][NA]  st2 st3 nei2 nei4 nei3 (nei: reference 1-based)
   int32_t* b_int;  // [8][NB]  st1..4 nei1..4
-  int32_t* owner;  // [N] key of the unit that moves protein p (0-based)
+  int32_t* owner;  // [N] key (reference index of the lead protein) of the unit that moves slot p
+  int32_t* id_of;    // [N] slot -> reference protein index (0-based)
+  int32_t* slot_of;  // [N] reference protein index -> slot
   uint8_t* ukind;  // [N] unit kind keyed at p
   uint32_t* ustate;  // [N] (step<<2)|S this step; older tag = accepted
   uint32_t* moved;   // [N] step tag (main.cpp:122)
@@ -127,8 +129,9 @@ __global__ void k_classify(KParams P, Dev d) {
       own = p;
     } else if (n2 == 0 && n3 != 0 && A_NEI3(d, n3 - 1) == i + 1 && A_NEI2(d, n3 - 1) == 0) {
       int q = n3 - 1;
-      own = i < q ? i : q;
-      kind = i < q ? U_DIMER : U_NONE;
+      const bool lead = d.id_of[i] < d.id_of[q];  // moved at the lower reference index
+      own = lead ? i : q;
+      kind = lead ? U_DIMER : U_NONE;
     }
   } else {
     int b = p - NA;
@@ -138,7 +141,7 @@ __global__ void k_classify(KParams P, Dev d) {
     }
   }
   d.ukind[p] = kind;
-  d.owner[p] = own;  // -1: complex member, set by the BFS kernels
+  d.owner[p] = own < 0 ? -1 : d.id_of[own];  // -1: complex member, set by the BFS kernels
 }
 
 // ================================================================ BFS
@@ -176,7 +179,7 @@ __device__ void register_complex(const KParams& P, const Dev& d, int p, const in
   for (int t = 0; t < qn; ++t) {
     int m = q[t];
     d.members[off + t] = m;
-    d.owner[m] = p;
+    d.owner[m] = d.id_of[p];
     nb += m >= P.NA;
   }
   int b = p - P.NA;
@@ -193,6 +196,7 @@ __global__ void k_bfs(KParams P, Dev d) {
   if (b >= NB) return;
   if (B_NEI(d, b, 2) == 0 && B_NEI(d, b, 3) == 0 && B_NEI(d, b, 4) == 0) return;
   int p = NA + b;
+  const int pid = d.id_of[p];
   int q[BFS_QCAP];
   int qn = 0, head = 0;
   q[qn++] = p;
@@ -202,7 +206,7 @@ __global__ void k_bfs(KParams P, Dev d) {
     int ny = nbrs(P, d, x, y);
     for (int e = 0; e < ny; ++e) {
       int v = y[e];
-      if (v >= NA && v < p) return;  // a lower ligand roots this component
+      if (v >= NA && d.id_of[v] < pid) return;  // a lower ligand roots this component
       bool seen = false;
       for (int t = 0; t < qn; ++t) seen |= q[t] == v;
       if (seen) continue;
@@ -224,6 +228,7 @@ __global__ void k_bfs_overflow(KParams P, Dev d) {
   uint32_t n = d.ctl->n_overflow;
   for (uint32_t o = 0; o < n; ++o) {
     int p = NA + d.overflow[o];
+    const int pid = d.id_of[p];
     uint32_t tag = (uint32_t)(++d.ctl->vtag);
     int* q = d.bfs_queue;
     int qn = 0, head = 0;
@@ -236,7 +241,7 @@ __global__ void k_bfs_overflow(KParams P, Dev d) {
       int ny = nbrs(P, d, x, y);
       for (int e = 0; e < ny; ++e) {
         int v = y[e];
-        if (v >= NA && v < p) {
+        if (v >= NA && d.id_of[v] < pid) {
           root = false;
           break;
         }
@@ -253,8 +258,9 @@ __global__ void k_bfs_overflow(KParams P, Dev d) {
 // free receptor, main.cpp:584-635
 __device__ void propose_free_a(const KParams& P, const Dev& d, int i, uint32_t step) {
   double u0, u1, u2, u3;
-  kmcr::uniform2(P.key, kmcr::DOM_DIFF, (uint32_t)i, 0, step, 0, &u0, &u1);
-  kmcr::uniform2(P.key, kmcr::DOM_DIFF, (uint32_t)i, 0, step, 1, &u2, &u3);
+  const uint32_t ri = (uint32_t)d.id_of[i];
+  kmcr::uniform2(P.key, kmcr::DOM_DIFF, ri, 0, step, 0, &u0, &u1);
+  kmcr::uniform2(P.key, kmcr::DOM_DIFF, ri, 0, step, 1, &u2, &u3);
   double amp = P.amp_a * u0;
   double phai = u1 * 2 * P.pai;
   double dx = amp * kmcm::cos(phai), dy = amp * kmcm::sin(phai);
@@ -355,8 +361,9 @@ __device__ __forceinline__ bool bond_misaligned(const KParams& P, const Beads& N
 // cis dimer lead i with partner q, main.cpp:682-865 (proposal part)
 __device__ void propose_dimer(const KParams& P, const Dev& d, int i, int q, uint32_t step) {
   double u0, u1, u2, u3;
-  kmcr::uniform2(P.key, kmcr::DOM_DIFF, (uint32_t)i, 0, step, 0, &u0, &u1);
-  kmcr::uniform2(P.key, kmcr::DOM_DIFF, (uint32_t)i, 0, step, 1, &u2, &u3);
+  const uint32_t ri = (uint32_t)d.id_of[i];
+  kmcr::uniform2(P.key, kmcr::DOM_DIFF, ri, 0, step, 0, &u0, &u1);
+  kmcr::uniform2(P.key, kmcr::DOM_DIFF, ri, 0, step, 1, &u2, &u3);
   double amp = P.amp_cis * u0;
   double phai = u1 * 2 * P.pai;
   double dx = amp * kmcm::cos(phai), dy = amp * kmcm::sin(phai);
@@ -396,9 +403,10 @@ __device__ void propose_dimer(const KParams& P, const Dev& d, int i, int q, uint
 // single ligand, main.cpp:905-969
 __device__ void propose_free_b(const KParams& P, const Dev& d, int lb, int p, uint32_t step) {
   double u[6];
-  kmcr::uniform2(P.key, kmcr::DOM_DIFF, (uint32_t)p, 0, step, 0, &u[0], &u[1]);
-  kmcr::uniform2(P.key, kmcr::DOM_DIFF, (uint32_t)p, 0, step, 1, &u[2], &u[3]);
-  kmcr::uniform2(P.key, kmcr::DOM_DIFF, (uint32_t)p, 0, step, 2, &u[4], &u[5]);
+  const uint32_t rp = (uint32_t)d.id_of[p];
+  kmcr::uniform2(P.key, kmcr::DOM_DIFF, rp, 0, step, 0, &u[0], &u[1]);
+  kmcr::uniform2(P.key, kmcr::DOM_DIFF, rp, 0, step, 1, &u[2], &u[3]);
+  kmcr::uniform2(P.key, kmcr::DOM_DIFF, rp, 0, step, 2, &u[4], &u[5]);
   double amp = P.amp_b * u[0];
   double theta = u[1] * P.pai;
   double phai = u[2] * 2 * P.pai;
@@ -462,7 +470,8 @@ struct Cx {
   const KParams& P;
   const Dev& d;
   uint32_t step;
-  int root;  // protein index of the root ligand
+  int root;  // slot of the root ligand
+  uint32_t rootid;  // its reference index (random stream key)
   int* res;  // member row (BFS order, shuffled in place like results[c][.])
   int size;
   __device__ bool isA(int m) const { return m < P.NA; }
@@ -484,7 +493,7 @@ struct Cx {
   __device__ bool is_moved(int m) const { return d.moved[m] == step + 1; }
   __device__ void set_moved(int m) const { d.moved[m] = step + 1; }
   __device__ uint32_t shuf_rand(uint32_t call, uint32_t pos) const {
-    return kmcr::rand31(P.key, kmcr::DOM_SHUF, (uint32_t)root, call, step, pos);
+    return kmcr::rand31(P.key, kmcr::DOM_SHUF, rootid, call, step, pos);
   }
   // libstdc++ random_shuffle over res[0 .. size-2] (main.cpp:1285)
   __device__ void shuffle(uint32_t call) const {
@@ -693,14 +702,14 @@ __global__ void k_complex(KParams P, Dev d) {
   if (d.ukind[p] != U_COMPLEX) return;
   const int NA = P.NA;
   const uint32_t step = d.ctl->step;
-  Cx X{P, d, step, p, d.members + d.cx_off[lb], d.cx_size[lb]};
+  Cx X{P, d, step, p, (uint32_t)d.id_of[p], d.members + d.cx_off[lb], d.cx_size[lb]};
   int* res = X.res;
   const int csize = X.size;
   int nB = d.cx_nb[lb], nA = csize - nB;
   // rigid move, main.cpp:974-1131
   double u0, u1, u2, u3;
-  kmcr::uniform2(P.key, kmcr::DOM_DIFF, (uint32_t)p, 0, step, 0, &u0, &u1);
-  kmcr::uniform2(P.key, kmcr::DOM_DIFF, (uint32_t)p, 0, step, 1, &u2, &u3);
+  kmcr::uniform2(P.key, kmcr::DOM_DIFF, X.rootid, 0, step, 0, &u0, &u1);
+  kmcr::uniform2(P.key, kmcr::DOM_DIFF, X.rootid, 0, step, 1, &u2, &u3);
   double amp = (nB == 1 ? P.amp_bond : 0.0) * u0;
   double phai = u1 * 2 * P.pai;
   double dx = amp * kmcm::cos(phai), dy = amp * kmcm::sin(phai);
@@ -1531,11 +1540,12 @@ __global__ void k_rxn_exact(KParams P, Dev d) {
                              N.A(i, 3, 1, 2) - N.A(i, 3, 4, 2), N.B(lb, 1, 1, 0) - N.B(lb, 1, 2, 0),
                              N.B(lb, 1, 1, 1) - N.B(lb, 1, 2, 1), N.B(lb, 1, 1, 2) - N.B(lb, 1, 2, 2));
         if (!((kmcm::fabs_(pd) < P.thetapd_cut) && (kmcm::fabs_(ot - 180) < P.thetaot_cut))) continue;
-        double u = kmcr::uniform(P.key, kmcr::DOM_RL, (uint32_t)i, (uint32_t)q, step, (uint32_t)k);
+        const uint64_t ri = (uint64_t)d.id_of[i], rq = (uint64_t)d.id_of[q];
+        double u = kmcr::uniform(P.key, kmcr::DOM_RL, (uint32_t)ri, (uint32_t)rq, step, (uint32_t)k);
         if (!(u < P.p_ass)) continue;
         uint32_t pos = atomicAdd(&d.ctl->n_rl, 1u);
         if (pos < d.cap_edges)
-          d.rl_keys[pos] = ((uint64_t)i << 34) | ((uint64_t)q << 2) | (uint64_t)(k - 2);
+          d.rl_keys[pos] = (ri << 34) | (rq << 2) | (uint64_t)(k - 2);
         else
           atomicOr(&d.ctl->err, ERR_EDGES);
       }
@@ -1547,13 +1557,14 @@ __global__ void k_rxn_exact(KParams P, Dev d) {
                            N.A(i, 3, 1, 2) - N.A(i, 3, 3, 2), N.A(q, 3, 1, 0) - N.A(q, 3, 3, 0),
                            N.A(q, 3, 1, 1) - N.A(q, 3, 3, 1), N.A(q, 3, 1, 2) - N.A(q, 3, 3, 2));
       if (!(kmcm::fabs_(ot - 180) < P.cis_theta_cut)) continue;
-      double um = kmcr::uniform(P.key, kmcr::DOM_MONO, (uint32_t)i, (uint32_t)q, step, 0);
-      double uc = kmcr::uniform(P.key, kmcr::DOM_CIS, (uint32_t)i, (uint32_t)q, step, 0);
+      const uint64_t ri = (uint64_t)d.id_of[i], rq = (uint64_t)d.id_of[q];
+      double um = kmcr::uniform(P.key, kmcr::DOM_MONO, (uint32_t)ri, (uint32_t)rq, step, 0);
+      double uc = kmcr::uniform(P.key, kmcr::DOM_CIS, (uint32_t)ri, (uint32_t)rq, step, 0);
       uint64_t fl = (um < P.p_mono ? 1u : 0u) | (uc < P.p_cis ? 2u : 0u);
       if (!fl) continue;
       uint32_t pos = atomicAdd(&d.ctl->n_cisc, 1u);
       if (pos < d.cap_edges)
-        d.cis_keys[pos] = ((uint64_t)i << 34) | ((uint64_t)q << 2) | fl;
+        d.cis_keys[pos] = (ri << 34) | (rq << 2) | fl;
       else
         atomicOr(&d.ctl->err, ERR_EDGES);
     }
@@ -1681,7 +1692,7 @@ __global__ void __launch_bounds__(1024) k_rl_match(KParams P, Dev d) {
   for (uint32_t e = threadIdx.x; e < n; e += blockDim.x) {
     if (!acc[e]) continue;
     uint64_t key = d.rl_keys[e];
-    int i = (int)(key >> 34), q = (int)((key >> 2) & 0xffffffffu), k = (int)(key & 3) + 2;
+    int i = d.slot_of[(int)(key >> 34)], q = d.slot_of[(int)((key >> 2) & 0xffffffffu)], k = (int)(key & 3) + 2;
     int lb = q - NA;
     A_ST2(d, i) = 1;
     B_ST(d, lb, k) = 1;
@@ -1707,7 +1718,7 @@ __global__ void __launch_bounds__(1024) k_cis_match(KParams P, Dev d) {
     __syncthreads();
     for (uint32_t t = threadIdx.x; t < n0; t += blockDim.x) {
       uint64_t key = keys[t];
-      int i = (int)(key >> 34), q = (int)((key >> 2) & 0xffffffffu);
+      int i = d.slot_of[(int)(key >> 34)], q = d.slot_of[(int)((key >> 2) & 0xffffffffu)];
       uint32_t fl = (uint32_t)(key & 3);
       bool unb = A_ST2(d, i) == 0 && A_ST2(d, q) == 0;
       bool ok = pass == 0 ? (unb && (fl & 1)) : (!unb && (fl & 2) && A_ST3(d, i) == 0 && A_ST3(d, q) == 0);
@@ -1723,7 +1734,7 @@ __global__ void __launch_bounds__(1024) k_cis_match(KParams P, Dev d) {
       block_greedy(n, e, CisV{}, d.ent, d.gi32, acc, &d.ctl->err);
       for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) {
         if (!acc[t]) continue;
-        int i = (int)(e[t] >> 34), q = (int)((e[t] >> 2) & 0xffffffffu);
+        int i = d.slot_of[(int)(e[t] >> 34)], q = d.slot_of[(int)((e[t] >> 2) & 0xffffffffu)];
         A_ST3(d, i) = 1;
         A_ST3(d, q) = 1;
         A_NEI3(d, q) = i + 1;
@@ -1741,7 +1752,7 @@ __global__ void k_diss_rl(KParams P, Dev d) {
   if (i >= NA) return;
   if (A_ST2(d, i) != 1) return;
   const uint32_t step = d.ctl->step;
-  double u = kmcr::uniform(P.key, kmcr::DOM_RLD, (uint32_t)i, 0, step, 0);
+  double u = kmcr::uniform(P.key, kmcr::DOM_RLD, (uint32_t)d.id_of[i], 0, step, 0);
   if (!(u < P.p_diss)) return;
   int q = A_NEI2(d, i) - 1, k = A_NEI4(d, i);
   int lb = q - NA;
@@ -1766,8 +1777,8 @@ __global__ void k_diss_cis(KParams P, Dev d) {
   bool mono = A_ST2(d, i) == 0 && A_ST2(d, q) == 0;
   uint32_t dom = mono ? kmcr::DOM_MD : kmcr::DOM_CD;
   double pd = mono ? P.p_mdiss : P.p_cdiss;
-  double ui = kmcr::uniform(P.key, dom, (uint32_t)i, 0, step, 0);
-  double uq = kmcr::uniform(P.key, dom, (uint32_t)q, 0, step, 0);
+  double ui = kmcr::uniform(P.key, dom, (uint32_t)d.id_of[i], 0, step, 0);
+  double uq = kmcr::uniform(P.key, dom, (uint32_t)d.id_of[q], 0, step, 0);
   if (ui < pd || uq < pd) {
     A_ST3(d, i) = 0;
     A_ST3(d, q) = 0;
@@ -1860,6 +1871,67 @@ __global__ void k_finalize(KParams P, Dev d, double time_step) {
   c->n_pairs = 0;
   c->rl = c->mono = c->cis = 0;
   c->tot_prot = c->tot_clu = c->max_size = 0;
+}
+
+
+// ================================================================ slot order
+// Proteins live in slots sorted by the tile-major cell of bead [1][1]
+// (receptors in [0, NA), ligands in [NA, N)), re-sorted every few hundred
+// steps, so that per-protein passes touch spatially coherent cache lines and
+// the cell-sorted records are written almost in order.  Nothing of the
+// simulation depends on the slot order: random streams, unit keys and the
+// reactions' greedy order use reference indices (id_of); bond fields hold
+// slot + 1 and are renumbered with the permutation.
+__device__ __forceinline__ uint32_t slot_key(const KParams& P, double x, double y) {
+  const int cx = cell_x(P, x), cy = cell_y(P, y), t = P.tile;
+  const int ntx = (P.ncx + t - 1) / t;
+  return ((uint32_t)((cy / t) * ntx + cx / t) * t + (uint32_t)(cy % t)) * t + (uint32_t)(cx % t);
+}
+
+__global__ void k_slot_keys(KParams P, Dev d, uint32_t* keys, int32_t* vals) {
+  int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= P.N) return;
+  double x = d.cur.P(s, 1, 1, 0), y = d.cur.P(s, 1, 1, 1);
+  keys[s] = slot_key(P, x, y);
+  vals[s] = s < P.NA ? s : s - P.NA;
+}
+
+// perm[s'] = old slot of new slot s' (sorted values, per kind); inverse map
+__global__ void k_slot_inverse(KParams P, const int32_t* sorted, int32_t* perm, int32_t* newslot) {
+  int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= P.N) return;
+  int old = s < P.NA ? sorted[s] : P.NA + sorted[s];
+  perm[s] = old;
+  newslot[old] = s;
+}
+
+// rows of a [rows][n] array gathered through perm (offset: kind's first slot)
+__global__ void k_gather_f64(const double* in, double* out, const int32_t* perm, int off, int n, int rows) {
+  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (size_t)n * rows) return;
+  int r = (int)(t / n), s = (int)(t % n);
+  out[(size_t)r * n + s] = in[(size_t)r * n + (perm[off + s] - off)];
+}
+
+// bond/state rows; rows flagged in link_mask hold protein index + 1 (0 = none)
+// and are renumbered through map
+__global__ void k_gather_i32(const int32_t* in, int32_t* out, const int32_t* perm, int off, int n, int rows,
+                             uint32_t link_mask, const int32_t* map) {
+  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (size_t)n * rows) return;
+  int r = (int)(t / n), s = (int)(t % n);
+  int v = in[(size_t)r * n + (perm[off + s] - off)];
+  if ((link_mask >> r & 1) && v > 0) v = map[v - 1] + 1;
+  out[(size_t)r * n + s] = v;
+}
+
+__global__ void k_gather_ids(KParams P, const int32_t* id_in, int32_t* id_out, int32_t* slot_of,
+                             const int32_t* perm) {
+  int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= P.N) return;
+  int id = id_in[perm[s]];
+  id_out[s] = id;
+  slot_of[id] = s;
 }
 
 }  // namespace kmcd

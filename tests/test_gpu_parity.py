@@ -108,6 +108,23 @@ def test_global_tile_path_dense(monkeypatch, tcap):
     assert engine.state_hash(p, sim.get_state()) == o.hash()
 
 
+def test_frequent_slot_resort_dense(monkeypatch):
+    # slots re-sorted every 7 steps while bonds form and break: bond fields,
+    # random-stream keys and unit keys must survive the renumbering
+    monkeypatch.setenv("KMC_RESORT", "7")
+    p = params(seed=29, **DENSE)
+    o = O.Oracle(p)
+    o.init_placement()
+    sim = engine.Simulation(p)
+    sim.set_state(o.get_state())
+    obs = sim.step(2000)
+    obs_o, _ = o.step(2000, want_hashes=False)
+    assert np.array_equal(obs, obs_o)
+    assert engine.state_hash(p, sim.get_state()) == o.hash()
+    st = o.stats()
+    assert st["rl"] > 0 and st["complex"] > 0
+
+
 def test_chunked_steps_equal_single_steps():
     p = params(seed=3, **DENSE)
     o = O.Oracle(p)
