@@ -45,6 +45,7 @@ struct Ctl {
   uint32_t n_conf;        // conflict entries (pass B)
   uint32_t n_plist;       // units with conflict entries
   uint32_t n_pend;        // units still pending after a round (pass C)
+  uint32_t n_rej;         // units rejected this step
   uint32_t n_rl;          // R–L accepting edges
   uint32_t n_cisc;        // cis candidates
   uint32_t n_pairs;       // reaction (receptor, record) pairs

@@ -20,13 +20,13 @@ using namespace kmcd;
 // kernel ids for per-kernel HIP-event timing (kmc_set_timing / kmc_kernel_times)
 enum KId {
   KI_CLASSIFY, KI_BFS, KI_BFS_OVF, KI_PROPOSE, KI_COMPLEX, KI_REC_COUNT, KI_SCAN, KI_REC_SCATTER,
-  KI_COL_SCAN, KI_COL_EXACT, KI_COL_ROUNDS, KI_COMMIT, KI_RXN_SCAN, KI_RXN_EXACT, KI_RL_MATCH, KI_CIS_MATCH, KI_DISS_RL,
-  KI_DISS_CIS, KI_OBSERVE, KI_FINALIZE, KI_RESORT, KI_N
+  KI_COL_SCAN, KI_COL_EXACT, KI_COL_ROUNDS, KI_COMMIT, KI_RXN_SCAN, KI_RXN_EXACT, KI_MATCH, KI_DISS, KI_OBSERVE,
+  KI_RESORT, KI_N
 };
 static const char* const KNAMES[KI_N] = {
     "k_classify", "k_bfs", "k_bfs_overflow", "k_propose", "k_complex", "k_rec_count", "k_scan",
     "k_rec_scatter", "k_col_scan", "k_col_exact", "k_col_rounds", "k_commit", "k_rxn_scan", "k_rxn_exact",
-    "k_rl_match", "k_cis_match", "k_diss_rl", "k_diss_cis", "k_observe", "k_finalize", "slot_resort"};
+    "k_match", "k_diss", "k_observe", "slot_resort"};
 #define TRING 64  // steps of event pairs kept in flight
 
 struct kmc_sim {
@@ -35,6 +35,8 @@ struct kmc_sim {
   Dev d;
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t side = nullptr;          // k_complex runs here, overlapping k_propose
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int64_t step_done = 0;
   std::string err;
   int ncell = 0, nscan_blocks = 0;
@@ -131,8 +133,11 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
     delete s;
     return KMC_ERR_NODEVICE;
   }
-  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
-    delete s;
+  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming) != hipSuccess) {
+    kmc_destroy(s);
     return KMC_ERR_HIP;
   }
   KParams& K = s->K;
@@ -226,7 +231,10 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   rc |= dalloc(s, &d.conf, d.cap_cand);
   d.cap_pairs = pow2(std::max<uint32_t>(1u << 16, (uint32_t)N));
   rc |= dalloc(s, &d.pairs, d.cap_pairs);
-  rc |= dalloc(s, &d.rfinal, N);
+  rc |= dalloc(s, &d.rejtag, N);
+  rc |= dalloc(s, &d.rej, N);
+  rc |= dalloc(s, &d.rank, N);
+  rc |= dalloc(s, &d.obs_part, (size_t)8 * ((N + 255) / 256));
   rc |= dalloc(s, &d.rl_keys, cap);
   rc |= dalloc(s, &d.cis_keys, cap);
   rc |= dalloc(s, &d.ent, (size_t)2 * cap);
@@ -285,12 +293,16 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
 int kmc_destroy(kmc_sim* s) {
   if (!s) return KMC_OK;
   if (s->stream) (void)hipStreamSynchronize(s->stream);
+  if (s->side) (void)hipStreamSynchronize(s->side);
   for (void* v : s->allocs) (void)hipFree(v);
   if (s->obs_buf) (void)hipFree(s->obs_buf);
   if (s->ctl_host) (void)hipHostFree(s->ctl_host);
   for (auto& e : s->tev)
     if (e) (void)hipEventDestroy(e);
   if (s->stream) (void)hipStreamDestroy(s->stream);
+  if (s->side) (void)hipStreamDestroy(s->side);
+  if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);
+  if (s->ev_join) (void)hipEventDestroy(s->ev_join);
   delete s;
   return KMC_OK;
 }
@@ -373,6 +385,7 @@ int kmc_set_state(kmc_sim* s, const kmc_state_view* v) {
   HIPCHK(s, hipMemcpy(d.ctl, &c, sizeof c, hipMemcpyHostToDevice));
   HIPCHK(s, hipMemset(d.ustate, 0, sizeof(uint32_t) * (size_t)(NA + NB)));
   HIPCHK(s, hipMemset(d.moved, 0, sizeof(uint32_t) * (size_t)(NA + NB)));
+  HIPCHK(s, hipMemset(d.rejtag, 0, sizeof(uint32_t) * (size_t)(NA + NB)));
   // reference order = identity slots, then the spatial sort
   k_iota<<<(NA + NB + 255) / 256, 256, 0, s->stream>>>(d.id_of, d.slot_of, NA + NB);
   rc = resort(s);
@@ -460,21 +473,27 @@ static void harvest(kmc_sim* s, int slot) {
 struct Bracket {
   kmc_sim* s;
   int k;
-  Bracket(kmc_sim* s_, int k_) : s(s_), k(k_) {
-    if (s->tmask >> k & 1) (void)hipEventRecord(s->tev[2 * ((size_t)s->tslot * KI_N + k)], s->stream);
+  hipStream_t st;
+  Bracket(kmc_sim* s_, int k_, hipStream_t st_) : s(s_), k(k_), st(st_) {
+    if (s->tmask >> k & 1) (void)hipEventRecord(s->tev[2 * ((size_t)s->tslot * KI_N + k)], st);
   }
   ~Bracket() {
     if (s->tmask >> k & 1) {
       size_t i = (size_t)s->tslot * KI_N + k;
-      (void)hipEventRecord(s->tev[2 * i + 1], s->stream);
+      (void)hipEventRecord(s->tev[2 * i + 1], st);
       s->tused[i] = 1;
     }
   }
 };
-#define TIMED(k, ...) \
-  do {                \
-    Bracket b_(s, k); \
-    __VA_ARGS__;      \
+#define TIMED(k, ...)            \
+  do {                           \
+    Bracket b_(s, k, s->stream); \
+    __VA_ARGS__;                 \
+  } while (0)
+#define TIMED_ON(k, stream, ...) \
+  do {                           \
+    Bracket b_(s, k, stream);    \
+    __VA_ARGS__;                 \
   } while (0)
 
 static int launch_step(kmc_sim* s, bool re_sort) {
@@ -499,8 +518,15 @@ static int launch_step(kmc_sim* s, bool re_sort) {
     TIMED(KI_BFS, (k_bfs<<<gB, T, 0, st>>>(K, d)));
     TIMED(KI_BFS_OVF, (k_bfs_overflow<<<1, 64, 0, st>>>(K, d)));
   }
+  // complexes (few, latency-bound, disjoint proteins) overlap the proposals
+  if (K.NB > 0) {
+    (void)hipEventRecord(s->ev_fork, st);
+    (void)hipStreamWaitEvent(s->side, s->ev_fork, 0);
+    TIMED_ON(KI_COMPLEX, s->side, (k_complex<<<(K.NB + 63) / 64, 64, 0, s->side>>>(K, d)));
+    (void)hipEventRecord(s->ev_join, s->side);
+  }
   TIMED(KI_PROPOSE, (k_propose<<<gN, T, 0, st>>>(K, d)));
-  if (K.NB > 0) TIMED(KI_COMPLEX, (k_complex<<<(K.NB + 63) / 64, 64, 0, st>>>(K, d)));
+  if (K.NB > 0) (void)hipStreamWaitEvent(st, s->ev_join, 0);
   TIMED(KI_REC_COUNT, (k_rec_count<<<gN, T, 0, st>>>(K, d)));
   TIMED(KI_SCAN, {
     k_scan1<<<s->nscan_blocks, SCAN_T, 0, st>>>(d.cell_cnt, d.cell_start, d.block_sums, s->ncell);
@@ -513,23 +539,24 @@ static int launch_step(kmc_sim* s, bool re_sort) {
   TIMED(KI_COL_SCAN, (k_col_scan<<<ntiles, 256, 0, st>>>(K, d)));
   TIMED(KI_COL_EXACT, (k_col_exact<<<gX, T, 0, st>>>(K, d)));
   TIMED(KI_COL_ROUNDS, {
-    for (int r = 0; r < 2; ++r) {
-      k_col_round<<<gX, T, 0, st>>>(K, d, r);
-      k_col_units<<<gX, T, 0, st>>>(K, d, r);
-    }
-    k_col_tail<<<1, 1024, 0, st>>>(K, d, 2);
+    k_col_round<<<gX, T, 0, st>>>(K, d, 0);
+    k_col_units<<<gX, T, 0, st>>>(K, d, 0);
+    k_col_tail<<<1, 1024, 0, st>>>(K, d, 1);
   });
-  TIMED(KI_COMMIT, (k_commit<<<gN, T, 0, st>>>(K, d)));
+  TIMED(KI_COMMIT, {
+    k_rej_mark<<<gX, T, 0, st>>>(K, d);
+    k_commit<<<gN, T, 0, st>>>(K, d);
+  });
   if (K.NA > 0) {
     TIMED(KI_RXN_SCAN, (k_rxn_scan_tile<<<ntiles, 256, 0, st>>>(K, d)));
     TIMED(KI_RXN_EXACT, (k_rxn_exact<<<1024, T, 0, st>>>(K, d)));
-    TIMED(KI_RL_MATCH, (k_rl_match<<<1, 1024, 0, st>>>(K, d)));
-    TIMED(KI_CIS_MATCH, (k_cis_match<<<1, 1024, 0, st>>>(K, d)));
-    TIMED(KI_DISS_RL, (k_diss_rl<<<gA, T, 0, st>>>(K, d)));
-    TIMED(KI_DISS_CIS, (k_diss_cis<<<gA, T, 0, st>>>(K, d)));
+    TIMED(KI_MATCH, (k_match<<<1, 1024, 0, st>>>(K, d)));
+    TIMED(KI_DISS, (k_diss<<<gA, T, 0, st>>>(K, d)));
   }
-  TIMED(KI_OBSERVE, (k_observe<<<gN, T, 0, st>>>(K, d)));
-  TIMED(KI_FINALIZE, (k_finalize<<<1, 1, 0, st>>>(K, d, s->p.time_step)));
+  TIMED(KI_OBSERVE, {
+    k_observe<<<gN, T, 0, st>>>(K, d);
+    k_finalize<<<1, 256, 0, st>>>(K, d, s->p.time_step, gN);
+  });
   if (s->tmask) s->tslot = (s->tslot + 1) % TRING;
   // R_new becomes R (main.cpp:2164-2191): swap the bead buffers
   std::swap(d.cur, d.nxt);

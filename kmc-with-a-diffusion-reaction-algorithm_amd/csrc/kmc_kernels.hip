@@ -54,7 +54,10 @@ struct Dev {
   int2* conf;           // [cap_cand] conflict entries (u, kq | isnew<<31)
   uint32_t cap_cand;
   int2* pairs;          // [cap_pairs] reaction candidate (receptor, record)
-  uint8_t* rfinal;      // [N] 1 if the proposal record is the final position
+  uint32_t* rejtag;     // [N] step at which the slot's unit was rejected (final = old position)
+  int32_t* rej;         // [N] units (keys) rejected this step
+  int2* rank;           // [N] rank of the old / proposed record within its cell
+  int32_t* obs_part;    // [blocks][8] per-block observable partials
   uint32_t cap_pairs;
   uint64_t* rl_keys;    // [cap]
   uint64_t* cis_keys;   // [cap]
@@ -822,21 +825,24 @@ __device__ __forceinline__ bool extent_ok(const Beads& B, int p, int NA) {
   return true;
 }
 
+// cell occupancy; each record's rank within its cell is kept for the scatter
 __global__ void k_rec_count(KParams P, Dev d) {
   int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P.N) return;
   double x, y, zl, zh;
+  int2 rk;
   ref_point(d, d.cur, p, P.NA, x, y, zl, zh);
-  atomicAdd(&d.cell_cnt[cell_y(P, y) * P.ncx + cell_x(P, x)], 1);
+  rk.x = atomicAdd(&d.cell_cnt[cell_y(P, y) * P.ncx + cell_x(P, x)], 1);
   ref_point(d, d.nxt, p, P.NA, x, y, zl, zh);
-  atomicAdd(&d.cell_cnt[cell_y(P, y) * P.ncx + cell_x(P, x)], 1);
+  rk.y = atomicAdd(&d.cell_cnt[cell_y(P, y) * P.ncx + cell_x(P, x)], 1);
+  d.rank[p] = rk;
   if (!extent_ok(d.nxt, p, P.NA)) atomicOr(&d.ctl->err, ERR_GEOMETRY);
 }
 
 // exclusive scan of cell_cnt[0..n) into cell_start[0..n]; 3 kernels
 #define SCAN_T 1024
 #define SCAN_PER 4
-__global__ void k_scan1(const int32_t* in, int32_t* out, int32_t* sums, int n) {
+__global__ void k_scan1(int32_t* in, int32_t* out, int32_t* sums, int n) {
   __shared__ int32_t s[SCAN_T];
   int base = (blockIdx.x * SCAN_T + threadIdx.x) * SCAN_PER;
   int v[SCAN_PER];
@@ -844,6 +850,7 @@ __global__ void k_scan1(const int32_t* in, int32_t* out, int32_t* sums, int n) {
 #pragma unroll
   for (int q = 0; q < SCAN_PER; ++q) {
     v[q] = base + q < n ? in[base + q] : 0;
+    if (base + q < n) in[base + q] = 0;  // counts start from zero next step
     tot += v[q];
   }
   s[threadIdx.x] = tot;
@@ -900,11 +907,12 @@ __global__ void k_rec_scatter(KParams P, Dev d) {
   if (p >= P.N) return;
   int st = 0;
   if (p < NA) st = (A_ST2(d, p) ? RID_ST2 : 0) | (A_ST3(d, p) ? RID_ST3 : 0);
+  const int2 rk = d.rank[p];
   for (int w = 0; w < 2; ++w) {
     double x, y, zl, zh;
     ref_point(d, w ? d.nxt : d.cur, p, P.NA, x, y, zl, zh);
     int c = cell_y(P, y) * P.ncx + cell_x(P, x);
-    int pos = d.cell_start[c] + atomicSub(&d.cell_cnt[c], 1) - 1;  // leaves cell_cnt zeroed
+    int pos = d.cell_start[c] + (w ? rk.y : rk.x);
     const Beads& B = w ? d.nxt : d.cur;
     Rec rc;
     rc.pos = make_float4((float)x, (float)y, (float)zl, (float)zh);
@@ -1080,7 +1088,7 @@ __device__ __forceinline__ int halo_search(const int* a, int stride, int v, int 
 // Returns false (uniformly) when the tile holds more than P.tcap records; the
 // caller then takes the global-memory path.  site (reaction scan only): the
 // [3][3] site of each record; its final flag goes into id.x as RID_FIN.
-__device__ bool tile_load(const KParams& P, const Dev& d, int tx, int ty, TileLds& T, float2* site) {
+__device__ bool tile_load(const KParams& P, const Dev& d, int tx, int ty, TileLds& T, float2* site, uint32_t step) {
   const int tile = P.tile, halo = tile + 2;
   const int cx0 = tx * tile - 1, cy0 = ty * tile - 1;
   const int xlo = max(cx0, 0), xhi = min(cx0 + halo - 1, P.ncx - 1);
@@ -1133,7 +1141,7 @@ __device__ bool tile_load(const KParams& P, const Dev& d, int tx, int ty, TileLd
         int2 id = rc[k].id;
         if (site) {
           site[l] = rc[k].site;
-          if ((id.x < 0) == (d.rfinal[id.x & RID_PID] != 0)) id.x |= RID_FIN;
+          if ((id.x < 0) != (d.rejtag[id.x & RID_PID] == step)) id.x |= RID_FIN;
         }
         T.pos[l] = rc[k].pos;
         T.id[l] = id;
@@ -1242,7 +1250,7 @@ __global__ void __launch_bounds__(256) k_col_scan(KParams P, Dev d) {
   const int ntx = (P.ncx + P.tile - 1) / P.tile;
   const int tx = blockIdx.x % ntx, ty = blockIdx.x / ntx;
   wg_list_init(L);
-  if (tile_load(P, d, tx, ty, T, nullptr)) {
+  if (tile_load(P, d, tx, ty, T, nullptr, 0)) {
     tile_items(P, T, [](int2 id) { return id.x < 0; });  // proposal records
     const int ni = T.nitem;
     for (int w = threadIdx.x; w < ni; w += blockDim.x) {
@@ -1273,6 +1281,12 @@ __global__ void __launch_bounds__(256) k_col_scan(KParams P, Dev d) {
 }
 
 // ---------------------------------------------------------------- 4b. exact
+// u rejected; the first to reject it lists it for the commit
+__device__ __forceinline__ void mark_rej(const Dev& d, int u, uint32_t tag) {
+  uint32_t old = atomicMax(&d.ustate[u], tag | S_REJ);
+  if (old != (tag | S_REJ)) d.rej[atomicAdd(&d.ctl->n_rej, 1u)] = u;  // at most once per unit: capacity N
+}
+
 // Pass B: exact fp64 overlap test of each candidate (main.cpp:640-664,
 // 1798-1826).  A collision with a record whose relevance is already known
 // (own unit, or a later unit's old position) rejects u outright; one with an
@@ -1291,7 +1305,7 @@ __global__ void k_col_exact(KParams P, Dev d) {
     load_own(P, d.nxt, m, o);
     if (!exact_collide(P, o, isnew ? d.nxt : d.cur, q)) continue;
     if (kq >= u) {
-      atomicMax(&d.ustate[u], tag | S_REJ);
+      mark_rej(d, u, tag);
       continue;
     }
     uint32_t old = atomicMax(&d.ustate[u], tag | S_PEND);
@@ -1322,7 +1336,7 @@ __device__ __forceinline__ void conf_entry(const Dev& d, int2 e, uint32_t step, 
   if (state_of(d, u, step) != S_PEND) return;
   uint32_t sk = state_of(d, kq, step);
   if (sk == S_PEND) st_state(&d.pend[u], rt);
-  else if ((sk == S_ACC) == isnew) atomicMax(&d.ustate[u], ((step & 0x3fffffffu) << 2) | S_REJ);
+  else if ((sk == S_ACC) == isnew) mark_rej(d, u, (step & 0x3fffffffu) << 2);
 }
 
 // returns 1 if u is still pending after this round
@@ -1380,17 +1394,30 @@ __global__ void __launch_bounds__(1024) k_col_tail(KParams P, Dev d, int round0)
 }
 
 // ================================================================ 5. commit
+// The members of every rejected unit get this step's reject tag (their final
+// position is the old one); untouched units were accepted.
+__global__ void k_rej_mark(KParams P, Dev d) {
+  const int NA = P.NA;
+  const uint32_t step = d.ctl->step;
+  const uint32_t n = d.ctl->n_rej;
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+    const int sl = d.slot_of[d.rej[t]];
+    const uint8_t kind = d.ukind[sl];
+    if (kind == U_COMPLEX) {
+      const int lb = sl - NA, off = d.cx_off[lb], cs = d.cx_size[lb];
+      for (int k = 0; k < cs; ++k) d.rejtag[d.members[off + k]] = step;
+    } else {
+      d.rejtag[sl] = step;
+      if (kind == U_DIMER) d.rejtag[A_NEI3(d, sl) - 1] = step;
+    }
+  }
+}
+
+// rejected proteins: R_new = R
 __global__ void k_commit(KParams P, Dev d) {
   int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P.N) return;
-  const uint32_t step = d.ctl->step;
-  uint32_t s = state_of(d, d.owner[p], step);
-  d.rfinal[p] = s == S_ACC;
-  if (s == S_ACC) return;
-  if (s != S_REJ) {
-    atomicOr(&d.ctl->err, ERR_RESOLVE);
-    return;
-  }
+  if (d.rejtag[p] != d.ctl->step) return;
   if (p < P.NA) {
     for (int r = 0; r < 48; ++r) d.nxt.a[(size_t)r * P.NA + p] = d.cur.a[(size_t)r * P.NA + p];
   } else {
@@ -1400,8 +1427,8 @@ __global__ void k_commit(KParams P, Dev d) {
 }
 
 // ================================================================ 6. reactions
-__device__ __forceinline__ bool record_final(const Dev& d, int2 id) {
-  return (id.x < 0) == (d.rfinal[id.x & RID_PID] != 0);
+__device__ __forceinline__ bool record_final(const Dev& d, int2 id, uint32_t step) {
+  return (id.x < 0) != (d.rejtag[id.x & RID_PID] == step);
 }
 
 // Reaction candidates, pass 1 (tiled): the final-position record of every
@@ -1416,7 +1443,7 @@ __device__ __forceinline__ void rxn_emit(const Dev& d, WgList& L, int i, int q) 
 
 // one receptor record, records from global memory (dense tiles)
 __device__ __forceinline__ void rxn_scan_glb(const KParams& P, const Dev& d, WgList& L, const int* r0, const int* r1,
-                                             int2 me, float4 mp, float2 ms) {
+                                             int2 me, float4 mp, float2 ms, uint32_t step) {
   const int NA = P.NA, NB = P.NB;
   const int i = me.x & RID_PID;
   const bool want_rl = !(me.x & RID_ST2) && NB > 0;
@@ -1442,7 +1469,7 @@ __device__ __forceinline__ void rxn_scan_glb(const KParams& P, const Dev& d, WgL
         float tx = qs.x - ms.x, ty = qs.y - ms.y;
         if (!(tx * tx + ty * ty < 16.0f * 16.0f)) continue;
       }
-      if (!record_final(d, id)) continue;
+      if (!record_final(d, id, step)) continue;
       rxn_emit(d, L, i, q);
     }
   }
@@ -1481,8 +1508,9 @@ __global__ void __launch_bounds__(256) k_rxn_scan_tile(KParams P, Dev d) {
   const int ntx = (P.ncx + P.tile - 1) / P.tile;
   const int tx = blockIdx.x % ntx, ty = blockIdx.x / ntx;
   const int NA = P.NA;
+  const uint32_t step = d.ctl->step;
   wg_list_init(L);
-  if (tile_load(P, d, tx, ty, T, site)) {
+  if (tile_load(P, d, tx, ty, T, site, step)) {
     // final receptor records that can still react
     tile_items(P, T, [NA](int2 id) {
       return (id.x & RID_PID) < NA && !((id.x & RID_ST2) && (id.x & RID_ST3)) && (id.x & RID_FIN);
@@ -1506,8 +1534,8 @@ __global__ void __launch_bounds__(256) k_rxn_scan_tile(KParams P, Dev d) {
     int s0 = d.cell_start[y * P.ncx + x], s1 = d.cell_start[y * P.ncx + x + 1];
     for (int r = s0; r < s1; ++r) {
       int2 me = d.rec[r].id;
-      if ((me.x & RID_PID) >= NA || ((me.x & RID_ST2) && (me.x & RID_ST3)) || !record_final(d, me)) continue;
-      rxn_scan_glb(P, d, L, r0, r1, me, d.rec[r].pos, d.rec[r].site);
+      if ((me.x & RID_PID) >= NA || ((me.x & RID_ST2) && (me.x & RID_ST3)) || !record_final(d, me, step)) continue;
+      rxn_scan_glb(P, d, L, r0, r1, me, d.rec[r].pos, d.rec[r].site, step);
     }
   }
   wg_flush(L, &d.ctl->n_pairs, d.pairs, d.cap_pairs, &d.ctl->err);
@@ -1678,7 +1706,7 @@ struct CisV {
 };
 
 // R–L association, main.cpp:1877-1949
-__global__ void __launch_bounds__(1024) k_rl_match(KParams P, Dev d) {
+__device__ void rl_match(const KParams& P, const Dev& d) {
   const int NA = P.NA, NB = P.NB;
   uint32_t n = d.ctl->n_rl;
   if (n == 0) return;
@@ -1703,7 +1731,7 @@ __global__ void __launch_bounds__(1024) k_rl_match(KParams P, Dev d) {
 }
 
 // cis association: mono (main.cpp:1952-2003) then complex (2007-2058)
-__global__ void __launch_bounds__(1024) k_cis_match(KParams P, Dev d) {
+__device__ void cis_match(const KParams& P, const Dev& d) {
   const int NA = P.NA;
   uint32_t n0 = d.ctl->n_cisc;
   if (n0 == 0) return;
@@ -1745,36 +1773,11 @@ __global__ void __launch_bounds__(1024) k_cis_match(KParams P, Dev d) {
   }
 }
 
-// R–L dissociation, main.cpp:2063-2092 (one bond per receptor: independent)
-__global__ void k_diss_rl(KParams P, Dev d) {
-  const int NA = P.NA, NB = P.NB;
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= NA) return;
-  if (A_ST2(d, i) != 1) return;
-  const uint32_t step = d.ctl->step;
-  double u = kmcr::uniform(P.key, kmcr::DOM_RLD, (uint32_t)d.id_of[i], 0, step, 0);
-  if (!(u < P.p_diss)) return;
-  int q = A_NEI2(d, i) - 1, k = A_NEI4(d, i);
-  int lb = q - NA;
-  A_ST2(d, i) = 0;
-  B_ST(d, lb, k) = 0;
-  A_NEI2(d, i) = 0;
-  A_NEI4(d, i) = 0;
-  B_NEI(d, lb, k) = 0;
-}
-
 // cis dissociation, mono (main.cpp:2097-2117) and complex (2120-2141): both
 // members of a pair draw in index order, so a pair breaks iff either draw
 // succeeds; handled by the lower index
-__global__ void k_diss_cis(KParams P, Dev d) {
+__device__ __forceinline__ void cis_diss(const KParams& P, const Dev& d, int i, int q, bool mono, uint32_t step) {
   const int NA = P.NA;
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= NA) return;
-  if (A_ST3(d, i) != 1) return;
-  int q = A_NEI3(d, i) - 1;
-  if (q < i) return;
-  const uint32_t step = d.ctl->step;
-  bool mono = A_ST2(d, i) == 0 && A_ST2(d, q) == 0;
   uint32_t dom = mono ? kmcr::DOM_MD : kmcr::DOM_CD;
   double pd = mono ? P.p_mdiss : P.p_cdiss;
   double ui = kmcr::uniform(P.key, dom, (uint32_t)d.id_of[i], 0, step, 0);
@@ -1785,6 +1788,46 @@ __global__ void k_diss_cis(KParams P, Dev d) {
     A_NEI3(d, i) = 0;
     A_NEI3(d, q) = 0;
   }
+}
+
+// both association passes in one workgroup (the cis pass reads the R–L outcome)
+__global__ void __launch_bounds__(1024) k_match(KParams P, Dev d) {
+  rl_match(P, d);
+  __syncthreads();
+  cis_match(P, d);
+}
+
+// R–L dissociation draw of receptor i (bonded), main.cpp:2063-2092
+__device__ __forceinline__ bool rl_breaks(const KParams& P, const Dev& d, int i, uint32_t step) {
+  return kmcr::uniform(P.key, kmcr::DOM_RLD, (uint32_t)d.id_of[i], 0, step, 0) < P.p_diss;
+}
+
+// R–L dissociation (one bond per receptor: independent), then cis
+// dissociation with the R–L outcome (st2 only goes 1 -> 0, and its final
+// value is a function of the receptor's own draw, so a partner's value read
+// before or after its own update gives the same answer)
+__global__ void k_diss(KParams P, Dev d) {
+  const int NA = P.NA, NB = P.NB;
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= NA) return;
+  const uint32_t step = d.ctl->step;
+  int st2_i = A_ST2(d, i);
+  if (st2_i == 1 && rl_breaks(P, d, i, step)) {
+    int q = A_NEI2(d, i) - 1, k = A_NEI4(d, i);
+    int lb = q - NA;
+    A_ST2(d, i) = 0;
+    B_ST(d, lb, k) = 0;
+    A_NEI2(d, i) = 0;
+    A_NEI4(d, i) = 0;
+    B_NEI(d, lb, k) = 0;
+    st2_i = 0;
+  }
+  if (A_ST3(d, i) != 1) return;
+  int q = A_NEI3(d, i) - 1;
+  if (q < i) return;
+  int st2_q = A_ST2(d, q);
+  if (st2_q == 1 && rl_breaks(P, d, q, step)) st2_q = 0;
+  cis_diss(P, d, i, q, st2_i == 0 && st2_q == 0, step);
 }
 
 // ================================================================ 7. observables
@@ -1831,21 +1874,43 @@ __global__ void __launch_bounds__(256) k_observe(KParams P, Dev d) {
   if ((threadIdx.x & 63) == 0)
     for (int f = 0; f < 6; ++f) red[w][f] = v[f];
   __syncthreads();
-  if (threadIdx.x < 6) {
+  if (threadIdx.x < 6) {  // per-block partials, reduced by k_finalize
     int f = threadIdx.x, a = red[0][f];
     for (int ww = 1; ww < 4; ++ww) a = f == 5 ? max(a, red[ww][f]) : a + red[ww][f];
-    if (a) {
-      int* dst = f == 0 ? &d.ctl->rl : f == 1 ? &d.ctl->mono : f == 2 ? &d.ctl->cis : f == 3 ? &d.ctl->tot_prot
-                 : f == 4 ? &d.ctl->tot_clu : &d.ctl->max_size;
-      if (f == 5) atomicMax(dst, a);
-      else atomicAdd(dst, a);
-    }
+    d.obs_part[blockIdx.x * 8 + f] = a;
   }
 }
 
-// bond.dat record (main.cpp:2195-2202, 2251) and step advance
-__global__ void k_finalize(KParams P, Dev d, double time_step) {
+// bond.dat record (main.cpp:2195-2202, 2251) and step advance; one
+// workgroup reduces the observable partials of k_observe's nblk blocks
+__global__ void __launch_bounds__(256) k_finalize(KParams P, Dev d, double time_step, int nblk) {
+  __shared__ int red[4][6];
+  int v[6] = {0, 0, 0, 0, 0, 0};
+  for (int b = threadIdx.x; b < nblk; b += blockDim.x) {
+    const int4 lo = *(const int4*)&d.obs_part[b * 8];
+    const int2 hi = *(const int2*)&d.obs_part[b * 8 + 4];
+    v[0] += lo.x;
+    v[1] += lo.y;
+    v[2] += lo.z;
+    v[3] += lo.w;
+    v[4] += hi.x;
+    v[5] = max(v[5], hi.y);
+  }
+  for (int f = 0; f < 5; ++f) v[f] = wave_sum(v[f]);
+  v[5] = wave_max(v[5]);
+  if ((threadIdx.x & 63) == 0)
+    for (int f = 0; f < 6; ++f) red[threadIdx.x >> 6][f] = v[f];
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  for (int w = 1; w < (int)(blockDim.x >> 6); ++w)
+    for (int f = 0; f < 6; ++f) red[0][f] = f == 5 ? max(red[0][f], red[w][f]) : red[0][f] + red[w][f];
   Ctl* c = d.ctl;
+  c->rl = red[0][0];
+  c->mono = red[0][1];
+  c->cis = red[0][2];
+  c->tot_prot = red[0][3];
+  c->tot_clu = red[0][4];
+  c->max_size = red[0][5];
   if (c->max_size > c->maxc) c->maxc = c->max_size;
   kmc_obs_dev o;
   o.step = (int64_t)c->step;
@@ -1865,7 +1930,7 @@ __global__ void k_finalize(KParams P, Dev d, double time_step) {
   // per-step counters for the next step (the former k_begin)
   c->n_overflow = 0;
   c->cx_cursor = 0;
-  c->n_cand = c->n_conf = c->n_plist = c->n_pend = 0;
+  c->n_cand = c->n_conf = c->n_plist = c->n_pend = c->n_rej = 0;
   c->n_rl = 0;
   c->n_cisc = 0;
   c->n_pairs = 0;
