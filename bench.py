@@ -56,6 +56,25 @@ def kernel_bytes(name: str, n_a: int, n_b: int):
     return models.get(name)
 
 
+TRAFFIC_JSON = "profiles/traffic_C3.json"
+
+
+def pmc_traffic(kernel: str, workload: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
+    (FETCH_SIZE x2 + WRITE_SIZE, tools/pmc_traffic.py) of this same bench
+    command; None when no profile of this workload is committed."""
+    path = os.path.join(REPO, TRAFFIC_JSON)
+    if workload != "C3" or not os.path.exists(path):
+        return None
+    rec = json.load(open(path)).get(kernel_trace_name(kernel))
+    return rec["traffic_bytes"] if rec else None
+
+
+def kernel_trace_name(name: str) -> str:
+    # engine timing names -> the kernel symbol rocprof reports
+    return {"k_rxn_scan": "k_rxn_scan_tile"}.get(name, name)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -117,6 +136,7 @@ def main():
     avg_s = total_ms / 1e3 / max(launches, 1)
     kb = kernel_bytes(dom, p.n_a, p.n_b)
     achieved = (kb / avg_s / 1e9) if (kb and avg_s > 0) else None
+    traffic = pmc_traffic(dom, args.workload)
     step_b = workloads.step_bytes(p.n_a, p.n_b)
     ms_per_step = dt / args.steps * 1e3
 
@@ -159,7 +179,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": TRAFFIC_JSON if traffic is not None else None,
                 "bytes_per_launch": kb,
                 "avg_launch_ms": avg_s * 1e3,
                 "step_bytes": step_b,

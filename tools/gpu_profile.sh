@@ -23,6 +23,8 @@ run trace --kernel-trace --stats --output-format csv
 run fetch --kernel-trace --pmc FETCH_SIZE --output-format csv
 run write --kernel-trace --pmc WRITE_SIZE --output-format csv
 run sq --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES --output-format csv
+python3 "$root/tools/pmc_traffic.py" "$(find "$out/fetch" -name '*counter_collection.csv' -print -quit)" \
+  "$(find "$out/write" -name '*counter_collection.csv' -print -quit)" "$out/traffic.json"
 run tcc --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv
 run sq2 --kernel-trace --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv || true
 {
