@@ -30,6 +30,7 @@ struct KParams {
   kmcr::Key key;
   int tcap;  // LDS tile record capacity (<= TCAP; lowered only to test the global path)
   int tile;  // cells per tile side of the LDS scans (<= TILE_MAX)
+  int dbg_stage;  // debug timing only: stop the tile scans after stage 1 (load) / 2 (items); 0 = off
 };
 
 // per-step control block in device memory (replayable without host writes)

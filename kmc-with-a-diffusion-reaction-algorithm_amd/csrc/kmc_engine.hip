@@ -140,6 +140,13 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
     kmc_destroy(s);
     return KMC_ERR_HIP;
   }
+  // the neighbour search's cell size and float prefilter radii are derived
+  // for the reference's radii and cutoffs (DESIGN.md §cell list); smaller
+  // values only shrink every reach
+  if (p->ra_radius > 20.0 || p->rb_radius > 30.0 || p->bond_dist_cutoff > 18.0 || p->cis_dist_cutoff > 15.0) {
+    kmc_destroy(s);
+    return KMC_ERR_ARG;
+  }
   KParams& K = s->K;
   const int NA = p->n_a, NB = p->n_b, N = NA + NB;
   K.NA = NA;
@@ -184,7 +191,7 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   K.T_cis = sqrt_threshold(p->cis_dist_cutoff);
   K.key = kmcr::make_key(p->seed, p->replica);
 
-  s->ncell = K.ncx * K.ncy;
+  s->ncell = 2 * K.ncx * K.ncy;  // (row, kind, column) record cells
   s->nscan_blocks = (s->ncell + SCAN_T * SCAN_PER - 1) / (SCAN_T * SCAN_PER);
   Dev& d = s->d;
   d.cur.NA = d.nxt.NA = NA;
@@ -265,6 +272,8 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
     const char* te = getenv("KMC_TILE");
     if (te && *te) t = std::max(2, std::min(TILE_MAX, atoi(te)));
     K.tile = t;
+    const char* ds = getenv("KMC_DEBUG_SCAN_STAGE");
+    K.dbg_stage = ds && *ds ? atoi(ds) : 0;
   }
   {
     const uint64_t ntx = (K.ncx + K.tile - 1) / K.tile, nty = (K.ncy + K.tile - 1) / K.tile;

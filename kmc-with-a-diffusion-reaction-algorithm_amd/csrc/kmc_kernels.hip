@@ -825,6 +825,11 @@ __device__ __forceinline__ bool extent_ok(const Beads& B, int p, int NA) {
   return true;
 }
 
+// sort key of a record: (cell row, kind, cell column), see §LDS tiles
+__device__ __forceinline__ int rec_cell(const KParams& P, double x, double y, int kind) {
+  return (cell_y(P, y) * 2 + kind) * P.ncx + cell_x(P, x);
+}
+
 // cell occupancy; each record's rank within its cell is kept for the scatter
 __global__ void k_rec_count(KParams P, Dev d) {
   int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -832,9 +837,10 @@ __global__ void k_rec_count(KParams P, Dev d) {
   double x, y, zl, zh;
   int2 rk;
   ref_point(d, d.cur, p, P.NA, x, y, zl, zh);
-  rk.x = atomicAdd(&d.cell_cnt[cell_y(P, y) * P.ncx + cell_x(P, x)], 1);
+  const int kind = p >= P.NA;
+  rk.x = atomicAdd(&d.cell_cnt[rec_cell(P, x, y, kind)], 1);
   ref_point(d, d.nxt, p, P.NA, x, y, zl, zh);
-  rk.y = atomicAdd(&d.cell_cnt[cell_y(P, y) * P.ncx + cell_x(P, x)], 1);
+  rk.y = atomicAdd(&d.cell_cnt[rec_cell(P, x, y, kind)], 1);
   d.rank[p] = rk;
   if (!extent_ok(d.nxt, p, P.NA)) atomicOr(&d.ctl->err, ERR_GEOMETRY);
 }
@@ -911,7 +917,7 @@ __global__ void k_rec_scatter(KParams P, Dev d) {
   for (int w = 0; w < 2; ++w) {
     double x, y, zl, zh;
     ref_point(d, w ? d.nxt : d.cur, p, P.NA, x, y, zl, zh);
-    int c = cell_y(P, y) * P.ncx + cell_x(P, x);
+    int c = rec_cell(P, x, y, p >= NA);
     int pos = d.cell_start[c] + (w ? rk.y : rk.x);
     const Beads& B = w ? d.nxt : d.cur;
     Rec rc;
@@ -1007,7 +1013,7 @@ __device__ __forceinline__ bool prefilter(bool mA, float mx, float my, float mzl
 // (slots handed out per wave: one LDS atomic per emitting wave-instruction),
 // and one global atomicAdd per workgroup reserves the output range.  Entries
 // beyond the LDS buffer go straight to global memory.
-#define EBUF 512
+#define EBUF 256
 struct WgList {
   int2 buf[EBUF];
   uint32_t n;
@@ -1056,74 +1062,88 @@ __device__ __forceinline__ void wg_flush(WgList& L, uint32_t* gctr, int2* gout, 
 }
 
 // ---------------------------------------------------------------- LDS tiles
+// Records are sorted by (cell row, kind, cell column) — cell_index() — so the
+// records of one kind in a run of columns of one row are contiguous.
+//
 // A workgroup owns a tile×tile block of cells (tile chosen on the host from
-// the record density so that a block holds about 200 scanning records for
-// its 256 threads).  It stages the records of the block plus a one-cell halo
-// into LDS (a halo row of cells is one contiguous range of the cell-sorted
-// array; all loads are issued up front), lists the block's scanning records
-// as work items, and each thread scans one item's 3x3 cells from LDS.
+// the record density).  It stages the records of the block plus a one-cell
+// halo into LDS as 2·halo segments (one per halo row and kind; each one
+// contiguous range of the sorted array, all loads in flight at once) and tags
+// every staged record with its (segment, column).  Every scanning record of
+// the block then writes the LDS indices of the records in its cut stencil —
+// per neighbour kind, only the cells within that kind pair's reach of the
+// record (its offset inside its cell decides which side columns / rows can
+// hold a partner) — into an LDS pair list (one wave-level prefix sum + one
+// LDS atomic per wave), and the pairs are checked with every lane busy.  A
+// record whose pairs do not fit the list is scanned in place.
 #define TILE_MAX 16
 #define HALO_MAX (TILE_MAX + 2)
+#define NSEG_MAX (2 * HALO_MAX)
 #define TCAP 1024
+#define PCAP 2048
+#define PAIR_NONE 0xffffffffu
 #define RID_FIN (1 << 24)  // staged record is its protein's final position (reaction scan)
 struct TileLds {
   float4 pos[TCAP];
   int2 id[TCAP];
-  uint32_t item[TCAP];                 // work item: LDS record index | halo cell << 16
-  int cstart[HALO_MAX][HALO_MAX + 1];  // LDS index of each halo cell's first record; [hy][halo] = row end
-  int goff[HALO_MAX];                  // global record index − LDS index, per halo row
+  uint16_t tag[TCAP];                  // segment | column << 8 of each staged record
+  uint32_t pair[PCAP];                 // scanning record | neighbour record << 16 (LDS indices)
+  int cstart[NSEG_MAX][HALO_MAX + 1];  // segment = halo row * 2 + kind: LDS index of each cell's first record; [seg][halo] = end
+  int goff[NSEG_MAX];                  // global record index − LDS index, per segment
   int n;
-  uint32_t nitem;
+  uint32_t npair;
 };
 
-// largest i in [0, cnt) with a[i * stride] <= v  (non-decreasing, a[0] <= v, cnt <= 32)
-__device__ __forceinline__ int halo_search(const int* a, int stride, int v, int cnt) {
-  int i = 0;
-#pragma unroll
-  for (int s = 16; s; s >>= 1)
-    if (i + s < cnt && a[(i + s) * stride] <= v) i += s;
-  return i;
+__device__ __forceinline__ int cell_index(const KParams& P, int cx, int cy, int kind) {
+  return (cy * 2 + kind) * P.ncx + cx;
 }
+
+__device__ __forceinline__ int tile_global(const TileLds& T, int l) { return l + T.goff[T.tag[l] & 0xff]; }
 
 // Returns false (uniformly) when the tile holds more than P.tcap records; the
 // caller then takes the global-memory path.  site (reaction scan only): the
 // [3][3] site of each record; its final flag goes into id.x as RID_FIN.
 __device__ bool tile_load(const KParams& P, const Dev& d, int tx, int ty, TileLds& T, float2* site, uint32_t step) {
-  const int tile = P.tile, halo = tile + 2;
+  const int tile = P.tile, halo = tile + 2, nseg = 2 * halo;
   const int cx0 = tx * tile - 1, cy0 = ty * tile - 1;
   const int xlo = max(cx0, 0), xhi = min(cx0 + halo - 1, P.ncx - 1);
-  if (threadIdx.x == 0) T.nitem = 0;
-  for (int idx = threadIdx.x; idx < halo * (halo + 1); idx += blockDim.x) {
-    int hy = idx / (halo + 1), hx = idx - hy * (halo + 1);
-    int y = cy0 + hy;
+  if (threadIdx.x == 0) T.npair = 0;
+  for (int idx = threadIdx.x; idx < nseg * (halo + 1); idx += blockDim.x) {
+    int seg = idx / (halo + 1), hx = idx - seg * (halo + 1);
+    int y = cy0 + (seg >> 1);
     int v = 0;
     if (y >= 0 && y < P.ncy && xlo <= xhi) {
       int x = min(max(cx0 + hx, xlo), xhi + 1);
-      v = d.cell_start[y * P.ncx + x];
+      v = d.cell_start[cell_index(P, x, y, seg & 1)];
     }
-    T.cstart[hy][hx] = v;
+    T.cstart[seg][hx] = v;
   }
   __syncthreads();
-  if (threadIdx.x < 64) {  // row lengths -> LDS row bases (wave-0 inclusive scan)
-    int hy = threadIdx.x;
-    int len = hy < halo ? T.cstart[hy][halo] - T.cstart[hy][0] : 0;
+  if (threadIdx.x < 64) {  // segment lengths -> LDS segment bases (wave-0 inclusive scan)
+    int seg = threadIdx.x;
+    int len = seg < nseg ? T.cstart[seg][halo] - T.cstart[seg][0] : 0;
     int inc = len;
 #pragma unroll
-    for (int o = 1; o < 32; o <<= 1) {
+    for (int o = 1; o < 64; o <<= 1) {
       int t = __shfl_up(inc, o, 64);
-      if (hy >= o) inc += t;
+      if (seg >= o) inc += t;
     }
-    if (hy < halo) T.goff[hy] = T.cstart[hy][0] - (inc - len);
-    if (hy == halo - 1) T.n = inc;
+    if (seg < nseg) T.goff[seg] = T.cstart[seg][0] - (inc - len);
+    if (seg == nseg - 1) T.n = inc;
   }
   __syncthreads();
-  for (int idx = threadIdx.x; idx < halo * (halo + 1); idx += blockDim.x) {
-    int hy = idx / (halo + 1), hx = idx - hy * (halo + 1);
-    T.cstart[hy][hx] -= T.goff[hy];
+  for (int idx = threadIdx.x; idx < nseg * (halo + 1); idx += blockDim.x) {
+    int seg = idx / (halo + 1), hx = idx - seg * (halo + 1);
+    T.cstart[seg][hx] -= T.goff[seg];
   }
   __syncthreads();
   const int n = T.n;
   if (n > P.tcap) return false;
+  for (int idx = threadIdx.x; idx < nseg * halo; idx += blockDim.x) {  // tags: one thread per cell
+    int seg = idx / halo, hx = idx - seg * halo;
+    for (int l = T.cstart[seg][hx]; l < T.cstart[seg][hx + 1]; ++l) T.tag[l] = (uint16_t)(seg | hx << 8);
+  }
+  __syncthreads();
   // four records per thread in flight: loads from clamped indices first, then
   // the LDS stores (keeps the staging arrays in registers)
   for (int base = 0; base < n; base += 4 * blockDim.x) {
@@ -1131,8 +1151,7 @@ __device__ bool tile_load(const KParams& P, const Dev& d, int tx, int ty, TileLd
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       int l = min(base + k * (int)blockDim.x + (int)threadIdx.x, n - 1);
-      int hy = halo_search(&T.cstart[0][0], HALO_MAX + 1, l, halo);
-      rc[k] = d.rec[l + T.goff[hy]];
+      rc[k] = d.rec[tile_global(T, l)];
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -1152,48 +1171,133 @@ __device__ bool tile_load(const KParams& P, const Dev& d, int tx, int ty, TileLd
   return true;
 }
 
-// The block's interior records satisfying pred(id) become work items (all
-// threads call; ends with a barrier).
-template <class Pred>
-__device__ __forceinline__ void tile_items(const KParams& P, TileLds& T, Pred pred) {
-  const int tile = P.tile, halo = tile + 2;
-  for (int l = threadIdx.x; l < T.n; l += blockDim.x) {
-    int hy = halo_search(&T.cstart[0][0], HALO_MAX + 1, l, halo);
-    if (hy < 1 || hy > tile || l < T.cstart[hy][1] || l >= T.cstart[hy][tile + 1]) continue;
-    if (!pred(T.id[l])) continue;
-    int hx = halo_search(&T.cstart[hy][0], 1, l, halo);
-    T.item[wave_slot(&T.nitem)] = (uint32_t)l | (uint32_t)(hy * HALO_MAX + hx) << 16;
+// Record ranges of the neighbour kind `kind` around the record at (seg, hx),
+// float position (px, py), cut to the cells within `reach` of it: three row
+// ranges (empty when the row is out of reach).
+__device__ __forceinline__ void item_ranges(const KParams& P, const TileLds& T, int tx, int ty, int seg, int hx,
+                                           float px, float py, int kind, float reach, int* r0, int* r1) {
+  const int hy = seg >> 1;
+  const int cx = tx * P.tile - 1 + hx, cy = ty * P.tile - 1 + hy;
+  const float xb = (float)(P.gx0 + cx * P.cs), yb = (float)(P.gy0 + cy * P.cs), cs = (float)P.cs;
+  const int lo = hx - (px - xb < reach ? 1 : 0), hi = hx + (xb + cs - px < reach ? 1 : 0);
+  const bool down = py - yb < reach, up = yb + cs - py < reach;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int s = (hy - 1 + k) * 2 + kind;
+    const bool on = k == 1 || (k == 0 ? down : up);
+    r0[k] = on ? T.cstart[s][lo] : 0;
+    r1[k] = on ? T.cstart[s][hi + 1] : 0;
+  }
+}
+
+// Pair list of the block: rng(l, seg, hx, r0, r1) gives the six ranges
+// (kind 0 rows, kind 1 rows) of a scanning record l, or false;
+// ovf(l, r0, r1) scans a record whose pairs do not fit.  All threads call;
+// ends with a barrier.
+template <class Rng, class Ovf>
+__device__ __forceinline__ void tile_pairs(const KParams& P, TileLds& T, Rng rng, Ovf ovf) {
+  const int tile = P.tile, n = T.n, lane = __lane_id();
+  for (int base = 0; base < n; base += blockDim.x) {
+    const int l = base + threadIdx.x;
+    int r0[6], r1[6];
+    bool item = false;
+    int tot = 0;
+    if (l < n) {
+      const int tg = T.tag[l], seg = tg & 0xff, hx = tg >> 8, hy = seg >> 1;
+      if (hy >= 1 && hy <= tile && hx >= 1 && hx <= tile) item = rng(l, seg, hx, r0, r1);
+      if (item)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) tot += r1[k] - r0[k];
+    }
+    int inc = tot;  // wave-level prefix sum (every lane of the wave is here)
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      int t = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += t;
+    }
+    const int wtot = __shfl(inc, 63, 64);
+    uint32_t wbase = 0;
+    if (lane == 0 && wtot) wbase = atomicAdd(&T.npair, (uint32_t)wtot);
+    wbase = __shfl(wbase, 0, 64);
+    if (!item) continue;
+    uint32_t off = wbase + (uint32_t)(inc - tot);
+    if (off + tot <= PCAP) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k)
+        for (int r = r0[k]; r < r1[k]; ++r) T.pair[off++] = (uint32_t)l | (uint32_t)r << 16;
+    } else {
+      for (uint32_t s = off; s < min(off + (uint32_t)tot, (uint32_t)PCAP); ++s) T.pair[s] = PAIR_NONE;
+      ovf(l, r0, r1);
+    }
   }
   __syncthreads();
 }
 
-// the 3x3 record ranges of work item c (halo cell hy * HALO_MAX + hx)
-__device__ __forceinline__ void item_ranges(const TileLds& T, int c, int* r0, int* r1, int* go) {
-  const int hy = c / HALO_MAX, hx = c - hy * HALO_MAX;
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    r0[k] = T.cstart[hy - 1 + k][hx - 1];
-    r1[k] = T.cstart[hy - 1 + k][hx + 2];
-    if (go) go[k] = T.goff[hy - 1 + k];
+// Up to four (a, b) entries held in registers per lane while pairs are
+// checked; the lanes of a wave then reserve their slots with one LDS atomic.
+struct PairBuf {
+  int2 v0, v1, v2, v3;
+  int n;
+};
+__device__ __forceinline__ void pair_push(PairBuf& b, int2 v) {
+  b.v0 = b.n == 0 ? v : b.v0;
+  b.v1 = b.n == 1 ? v : b.v1;
+  b.v2 = b.n == 2 ? v : b.v2;
+  b.v3 = b.n == 3 ? v : b.v3;
+  ++b.n;
+}
+// active lanes of a wave; entries mapped through f on the way out
+template <class F>
+__device__ __forceinline__ void pair_flush(const PairBuf& b, WgList& L, uint32_t* gctr, int2* gout, uint32_t cap,
+                                           uint32_t* err, F f) {
+  const int n = min(b.n, 4);
+  const uint64_t lt = (1ull << __lane_id()) - 1ull;
+  const uint64_t b0 = __ballot(n & 1), b1 = __ballot(n & 2), b2 = __ballot(n & 4);
+  const uint32_t pre = __popcll(b0 & lt) + 2 * __popcll(b1 & lt) + 4 * __popcll(b2 & lt);
+  const uint32_t tot = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
+  if (tot == 0) return;
+  const int leader = __ffsll((unsigned long long)__ballot(1)) - 1;
+  uint32_t base = 0;
+  if (__lane_id() == leader) base = atomicAdd(&L.n, tot);
+  base = __shfl(base, leader, 64);
+  for (int k = 0; k < n; ++k) {
+    const int2 v = f(k == 0 ? b.v0 : k == 1 ? b.v1 : k == 2 ? b.v2 : b.v3);
+    const uint32_t s = base + pre + k;
+    if (s < EBUF) {
+      L.buf[s] = v;
+    } else {
+      uint32_t pos = atomicAdd(gctr, 1u);
+      if (pos < cap) gout[pos] = v;
+      else atomicOr(err, ERR_EDGES);
+    }
   }
 }
 
-// global-memory path (dense tile): the 3x3 record ranges of cell (x, y)
-__device__ __forceinline__ void cell_ranges(const KParams& P, const Dev& d, int x, int y, int* r0, int* r1) {
+// global-memory path (dense tile): the full 3x3 record ranges of one kind
+__device__ __forceinline__ void cell_ranges(const KParams& P, const Dev& d, int x, int y, int kind, int* r0, int* r1) {
   int x0 = max(x - 1, 0), x1 = min(x + 1, P.ncx - 1);
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     int yy = y - 1 + k;
     bool ok = yy >= 0 && yy < P.ncy;
-    r0[k] = ok ? d.cell_start[yy * P.ncx + x0] : 0;
-    r1[k] = ok ? d.cell_start[yy * P.ncx + x1 + 1] : 0;
+    r0[k] = ok ? d.cell_start[cell_index(P, x0, yy, kind)] : 0;
+    r1[k] = ok ? d.cell_start[cell_index(P, x1 + 1, yy, kind)] : 0;
   }
 }
 
+// reach (xy, Å) of the float prefilters per kind pair, + 1 Å for the float
+// cell bounds: receptor-receptor 42, receptor-ligand 86.5, ligand-ligand: any
+// collision has centres < 130 Å apart (DESIGN.md §cell list), i.e. all cells
+#define REACH_AA 43.0f
+#define REACH_AB 87.5f
+#define REACH_BB 131.0f
+#define REACH_RL 106.0f
+#define REACH_CIS 58.0f
+
 // ---------------------------------------------------------------- 4a. scan
 // Pass A: every proposal record (member m of unit u = its owner) is checked
-// against the records of its 3x3 cells.  The filters that do not depend on
-// any unit's fate are applied here (main.cpp:640-664 visits R_new, i.e. the
+// against the records of its cells.  The filters that do not depend on any
+// unit's fate are applied here (main.cpp:640-664 visits R_new, i.e. the
 // proposals of earlier units and the old positions of later ones):
 //   owner kq == u : only the unit's other proposal records
 //   owner kq >  u : only old-position records
@@ -1203,64 +1307,87 @@ __device__ __forceinline__ void col_emit(const Dev& d, WgList& L, int rs, int rg
   wg_emit(L, make_int2(rs, rg), &d.ctl->n_cand, d.cand, d.cap_cand, &d.ctl->err);
 }
 
-struct LdsRecs {
-  const float4* pos;
-  const int2* ids;
-  __device__ float4 p(int r) const { return pos[r]; }
-  __device__ int2 id(int r) const { return ids[r]; }
-};
+// the fate-independent filters + prefilter for one (proposal, record) pair
+__device__ __forceinline__ bool col_pair(int NA, int2 me, float4 mp, int2 id, float4 rp) {
+  const int m = me.x & RID_PID, u = me.y;
+  const int q = id.x & RID_PID, kq = id.y;
+  const bool isnew = id.x < 0;
+  const bool own_ok = kq == u ? isnew : (kq > u ? !isnew : true);
+  return (q != m) & own_ok & prefilter(m < NA, mp.x, mp.y, mp.z, mp.w, q < NA, rp);
+}
+
 struct GlbRecs {
   const Rec* rec;
   __device__ float4 p(int r) const { return rec[r].pos; }
   __device__ int2 id(int r) const { return rec[r].id; }
 };
 
-// src: record source (LDS or global); rows k=0..2: [r0[k], r1[k]) with
-// global index = r + goff[k].  The three row ranges are walked as one loop and
-// the filters are branch-free (lanes of a wave stay converged).
-template <class S>
-__device__ __forceinline__ void col_scan_rec(const KParams& P, const Dev& d, WgList& L, S src, const int* r0,
-                                             const int* r1, const int* goff, int rs, int2 me, float4 mp) {
-  const int NA = P.NA;
-  const int m = me.x & RID_PID, u = me.y;
-  if (u < 0) {
-    atomicOr(&d.ctl->err, ERR_RESOLVE);
-    return;
-  }
-  const bool mA = m < NA;
-  const int l0 = r1[0] - r0[0], l01 = l0 + r1[1] - r0[1], tot = l01 + r1[2] - r0[2];
-  for (int t = 0; t < tot; ++t) {
-    const bool k0 = t < l0, k1 = t < l01;
-    const int r = k0 ? r0[0] + t : (k1 ? r0[1] + (t - l0) : r0[2] + (t - l01));
-    const int2 id = src.id(r);
-    const float4 rp = src.p(r);
-    const int q = id.x & RID_PID, kq = id.y;
-    const bool isnew = id.x < 0;
-    const bool own_ok = kq == u ? isnew : (kq > u ? !isnew : true);
-    if ((q != m) & own_ok & prefilter(mA, mp.x, mp.y, mp.z, mp.w, q < NA, rp)) {
-      if (kq < 0) atomicOr(&d.ctl->err, ERR_RESOLVE);
-      else col_emit(d, L, rs, r + (k0 ? goff[0] : (k1 ? goff[1] : goff[2])));
+// one proposal record against three row ranges of records from global memory
+__device__ __forceinline__ void col_scan_glb(const KParams& P, const Dev& d, WgList& L, const int* r0, const int* r1,
+                                             int rs, int2 me, float4 mp) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+    for (int r = r0[k]; r < r1[k]; ++r) {
+      const int2 id = d.rec[r].id;
+      if (!col_pair(P.NA, me, mp, id, d.rec[r].pos)) continue;
+      if (id.y < 0) atomicOr(&d.ctl->err, ERR_RESOLVE);
+      else col_emit(d, L, rs, r);
     }
-  }
 }
 
 __global__ void __launch_bounds__(256) k_col_scan(KParams P, Dev d) {
   __shared__ TileLds T;
   __shared__ WgList L;
+  const int NA = P.NA;
   const int ntx = (P.ncx + P.tile - 1) / P.tile;
   const int tx = blockIdx.x % ntx, ty = blockIdx.x / ntx;
   wg_list_init(L);
   if (tile_load(P, d, tx, ty, T, nullptr, 0)) {
-    tile_items(P, T, [](int2 id) { return id.x < 0; });  // proposal records
-    const int ni = T.nitem;
-    for (int w = threadIdx.x; w < ni; w += blockDim.x) {
-      const uint32_t it = T.item[w];
-      const int l = it & 0xffff;
-      int r0[3], r1[3], go[3];
-      item_ranges(T, it >> 16, r0, r1, go);
-      const int hy = (it >> 16) / HALO_MAX;
-      col_scan_rec(P, d, L, LdsRecs{T.pos, T.id}, r0, r1, go, l + T.goff[hy], T.id[l], T.pos[l]);
+    if (P.dbg_stage == 1) return;
+    // proposal records and their cut stencils
+    tile_pairs(
+        P, T,
+        [&](int l, int seg, int hx, int* r0, int* r1) {
+          const int2 me = T.id[l];
+          if (me.x >= 0) return false;
+          if (me.y < 0) {
+            atomicOr(&d.ctl->err, ERR_RESOLVE);
+            return false;
+          }
+          const float4 mp = T.pos[l];
+          const bool mA = (me.x & RID_PID) < NA;
+          item_ranges(P, T, tx, ty, seg, hx, mp.x, mp.y, 0, mA ? REACH_AA : REACH_AB, r0, r1);
+          item_ranges(P, T, tx, ty, seg, hx, mp.x, mp.y, 1, mA ? REACH_AB : REACH_BB, r0 + 3, r1 + 3);
+          return true;
+        },
+        [&](int l, const int* r0, const int* r1) {
+          const int2 me = T.id[l];
+          const float4 mp = T.pos[l];
+          for (int k = 0; k < 6; ++k)
+            for (int r = r0[k]; r < r1[k]; ++r) {
+              const int2 id = T.id[r];
+              if (!col_pair(NA, me, mp, id, T.pos[r])) continue;
+              if (id.y < 0) atomicOr(&d.ctl->err, ERR_RESOLVE);
+              else col_emit(d, L, tile_global(T, l), tile_global(T, r));
+            }
+        });
+    if (P.dbg_stage == 2) return;
+    const uint32_t np = min(T.npair, (uint32_t)PCAP);
+    PairBuf B;
+    B.n = 0;
+    for (uint32_t p = threadIdx.x; p < np; p += blockDim.x) {
+      const uint32_t e = T.pair[p];
+      if (e == PAIR_NONE) continue;
+      const int il = e & 0xffff, nl = e >> 16;
+      const int2 id = T.id[nl];
+      if (!col_pair(NA, T.id[il], T.pos[il], id, T.pos[nl])) continue;
+      if (id.y < 0) atomicOr(&d.ctl->err, ERR_RESOLVE);
+      else if (B.n < 4) pair_push(B, make_int2(il, nl));
+      else col_emit(d, L, tile_global(T, il), tile_global(T, nl));
     }
+    pair_flush(B, L, &d.ctl->n_cand, d.cand, d.cap_cand, &d.ctl->err,
+               [&](int2 v) { return make_int2(tile_global(T, v.x), tile_global(T, v.y)); });
+    if (P.dbg_stage == 3) return;
     wg_flush(L, &d.ctl->n_cand, d.cand, d.cap_cand, &d.ctl->err);
     return;
   }
@@ -1268,13 +1395,21 @@ __global__ void __launch_bounds__(256) k_col_scan(KParams P, Dev d) {
   for (int c = threadIdx.x; c < P.tile * P.tile; c += blockDim.x) {
     int x = tx * P.tile + c % P.tile, y = ty * P.tile + c / P.tile;
     if (x >= P.ncx || y >= P.ncy) continue;
-    int r0[3], r1[3], go[3] = {0, 0, 0};
-    cell_ranges(P, d, x, y, r0, r1);
-    int s0 = d.cell_start[y * P.ncx + x], s1 = d.cell_start[y * P.ncx + x + 1];
-    for (int r = s0; r < s1; ++r) {
-      int2 me = d.rec[r].id;
-      if (me.x >= 0) continue;
-      col_scan_rec(P, d, L, GlbRecs{d.rec}, r0, r1, go, r, me, d.rec[r].pos);
+    int ra[3], rb[3], sa[3], sb[3];
+    cell_ranges(P, d, x, y, 0, ra, sa);
+    cell_ranges(P, d, x, y, 1, rb, sb);
+    for (int kind = 0; kind < 2; ++kind) {
+      int s0 = d.cell_start[cell_index(P, x, y, kind)], s1 = d.cell_start[cell_index(P, x + 1, y, kind)];
+      for (int r = s0; r < s1; ++r) {
+        int2 me = d.rec[r].id;
+        if (me.x >= 0) continue;
+        if (me.y < 0) {
+          atomicOr(&d.ctl->err, ERR_RESOLVE);
+          continue;
+        }
+        col_scan_glb(P, d, L, ra, sa, r, me, d.rec[r].pos);
+        col_scan_glb(P, d, L, rb, sb, r, me, d.rec[r].pos);
+      }
     }
   }
   wg_flush(L, &d.ctl->n_cand, d.cand, d.cap_cand, &d.ctl->err);
@@ -1432,73 +1567,43 @@ __device__ __forceinline__ bool record_final(const Dev& d, int2 id, uint32_t ste
 }
 
 // Reaction candidates, pass 1 (tiled): the final-position record of every
-// receptor that can still react scans the final records of its 3x3 cells
+// receptor that can still react is paired with the final records in its cut
+// stencil (cis: receptors within 58 Å, R–L: ligands within 106 Å) and checked
 // with conservative single-precision prefilters (R–L: ligand centre within
-// reach of the [3][2] site; cis: the two [3][3] sites within 16 Å) and emits
-// (receptor, partner) pairs; the exact gates run in pass 2.  Record sites
-// and final flags are staged in LDS with the tile.
+// reach of the [3][2] site; cis: the two [3][3] sites within 16 Å); passing
+// (receptor, partner) pairs go to the exact gates of pass 2.  Record sites and
+// final flags are staged in LDS with the tile.
 __device__ __forceinline__ void rxn_emit(const Dev& d, WgList& L, int i, int q) {
   wg_emit(L, make_int2(i, q), &d.ctl->n_pairs, d.pairs, d.cap_pairs, &d.ctl->err);
 }
 
-// one receptor record, records from global memory (dense tiles)
-__device__ __forceinline__ void rxn_scan_glb(const KParams& P, const Dev& d, WgList& L, const int* r0, const int* r1,
-                                             int2 me, float4 mp, float2 ms, uint32_t step) {
-  const int NA = P.NA, NB = P.NB;
-  const int i = me.x & RID_PID;
-  const bool want_rl = !(me.x & RID_ST2) && NB > 0;
-  const bool want_cis = !(me.x & RID_ST3);
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    for (int r = r0[k]; r < r1[k]; ++r) {
-      int2 id = d.rec[r].id;
-      int q = id.x & RID_PID;
-      if (q == i) continue;
-      float4 rp = d.rec[r].pos;
-      float dx = rp.x - mp.x, dy = rp.y - mp.y;
-      float dxy2 = dx * dx + dy * dy;
-      if (q >= NA) {
-        if (!want_rl) continue;
-        if (!(dxy2 < 105.0f * 105.0f) || !(rp.z > mp.z - 85.0f && rp.z < mp.w + 85.0f)) continue;
-      } else {
-        if (!want_cis || (id.x & RID_ST3)) continue;
-        if (!(dxy2 < 57.0f * 57.0f)) continue;
-        float gap = fmaxf(fmaxf(rp.z - mp.w, mp.z - rp.w), 0.0f);
-        if (!(gap < 16.0f)) continue;
-        float2 qs = d.rec[r].site;
-        float tx = qs.x - ms.x, ty = qs.y - ms.y;
-        if (!(tx * tx + ty * ty < 16.0f * 16.0f)) continue;
-      }
-      if (!record_final(d, id, step)) continue;
-      rxn_emit(d, L, i, q);
-    }
-  }
+// prefilter of one (receptor record, final-candidate record) pair
+__device__ __forceinline__ bool rxn_pair(int NA, int2 me, float4 mp, float2 ms, int2 id, float4 rp, float2 qs) {
+  const int i = me.x & RID_PID, q = id.x & RID_PID;
+  const bool isB = q >= NA;
+  const float dx = rp.x - mp.x, dy = rp.y - mp.y;
+  const float dxy2 = dx * dx + dy * dy;
+  const bool rl_ok = isB & (dxy2 < 105.0f * 105.0f) & (rp.z > mp.z - 85.0f) & (rp.z < mp.w + 85.0f);
+  const float gap = fmaxf(fmaxf(rp.z - mp.w, mp.z - rp.w), 0.0f);
+  const float tx = qs.x - ms.x, ty = qs.y - ms.y;
+  const bool cis_ok = !isB & !(id.x & RID_ST3) & (dxy2 < 57.0f * 57.0f) & (gap < 16.0f) &
+                      (tx * tx + ty * ty < 16.0f * 16.0f);
+  return (q != i) & (rl_ok | cis_ok);
 }
 
-__device__ __forceinline__ void rxn_scan_lds(const KParams& P, const Dev& d, WgList& L, const TileLds& T,
-                                             const float2* site, const int* r0, const int* r1, int2 me, float4 mp,
-                                             float2 ms) {
-  const int NA = P.NA, NB = P.NB;
-  const int i = me.x & RID_PID;
-  const bool want_rl = !(me.x & RID_ST2) && NB > 0;
-  const bool want_cis = !(me.x & RID_ST3);
-  const int l0 = r1[0] - r0[0], l01 = l0 + r1[1] - r0[1], tot = l01 + r1[2] - r0[2];
-  for (int t = 0; t < tot; ++t) {
-    const int r = t < l0 ? r0[0] + t : (t < l01 ? r0[1] + (t - l0) : r0[2] + (t - l01));
-    const int2 id = T.id[r];
-    const float4 rp = T.pos[r];
-    const float2 qs = site[r];
-    const int q = id.x & RID_PID;
-    const bool isB = q >= NA;
-    const float dx = rp.x - mp.x, dy = rp.y - mp.y;
-    const float dxy2 = dx * dx + dy * dy;
-    const bool rl_ok = isB & want_rl & (dxy2 < 105.0f * 105.0f) & (rp.z > mp.z - 85.0f) & (rp.z < mp.w + 85.0f);
-    const float gap = fmaxf(fmaxf(rp.z - mp.w, mp.z - rp.w), 0.0f);
-    const float tx = qs.x - ms.x, ty = qs.y - ms.y;
-    const bool cis_ok = !isB & want_cis & !(id.x & RID_ST3) & (dxy2 < 57.0f * 57.0f) & (gap < 16.0f) &
-                        (tx * tx + ty * ty < 16.0f * 16.0f);
-    if ((q != i) & (rl_ok | cis_ok) & ((id.x & RID_FIN) != 0)) rxn_emit(d, L, i, q);
-  }
+// one receptor record against three row ranges, records from global memory
+__device__ __forceinline__ void rxn_scan_glb(const KParams& P, const Dev& d, WgList& L, const int* r0, const int* r1,
+                                             int2 me, float4 mp, float2 ms, uint32_t step) {
+  const bool want_rl = !(me.x & RID_ST2) && P.NB > 0, want_cis = !(me.x & RID_ST3);
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+    for (int r = r0[k]; r < r1[k]; ++r) {
+      const int2 id = d.rec[r].id;
+      const int q = id.x & RID_PID;
+      if (!(q >= P.NA ? want_rl : want_cis)) continue;
+      if (!rxn_pair(P.NA, me, mp, ms, id, d.rec[r].pos, d.rec[r].site) || !record_final(d, id, step)) continue;
+      rxn_emit(d, L, me.x & RID_PID, q);
+    }
 }
 
 __global__ void __launch_bounds__(256) k_rxn_scan_tile(KParams P, Dev d) {
@@ -1507,35 +1612,66 @@ __global__ void __launch_bounds__(256) k_rxn_scan_tile(KParams P, Dev d) {
   __shared__ WgList L;
   const int ntx = (P.ncx + P.tile - 1) / P.tile;
   const int tx = blockIdx.x % ntx, ty = blockIdx.x / ntx;
-  const int NA = P.NA;
+  const int NA = P.NA, NB = P.NB;
   const uint32_t step = d.ctl->step;
   wg_list_init(L);
   if (tile_load(P, d, tx, ty, T, site, step)) {
-    // final receptor records that can still react
-    tile_items(P, T, [NA](int2 id) {
-      return (id.x & RID_PID) < NA && !((id.x & RID_ST2) && (id.x & RID_ST3)) && (id.x & RID_FIN);
-    });
-    const int ni = T.nitem;
-    for (int w = threadIdx.x; w < ni; w += blockDim.x) {
-      const uint32_t it = T.item[w];
-      const int l = it & 0xffff;
-      int r0[3], r1[3];
-      item_ranges(T, it >> 16, r0, r1, nullptr);
-      rxn_scan_lds(P, d, L, T, site, r0, r1, T.id[l], T.pos[l], site[l]);
+    if (P.dbg_stage == 1) return;
+    // final receptor records that can still react, and their cut stencils
+    tile_pairs(
+        P, T,
+        [&](int l, int seg, int hx, int* r0, int* r1) {
+          const int2 me = T.id[l];
+          if ((me.x & RID_PID) >= NA || ((me.x & RID_ST2) && (me.x & RID_ST3)) || !(me.x & RID_FIN)) return false;
+          const float4 mp = T.pos[l];
+          item_ranges(P, T, tx, ty, seg, hx, mp.x, mp.y, 0, REACH_CIS, r0, r1);
+          item_ranges(P, T, tx, ty, seg, hx, mp.x, mp.y, 1, REACH_RL, r0 + 3, r1 + 3);
+          if (me.x & RID_ST3)
+            for (int k = 0; k < 3; ++k) r1[k] = r0[k];
+          if ((me.x & RID_ST2) || NB == 0)
+            for (int k = 3; k < 6; ++k) r1[k] = r0[k];
+          return true;
+        },
+        [&](int l, const int* r0, const int* r1) {
+          const int2 me = T.id[l];
+          for (int k = 0; k < 6; ++k)
+            for (int r = r0[k]; r < r1[k]; ++r) {
+              const int2 id = T.id[r];
+              if (rxn_pair(NA, me, T.pos[l], site[l], id, T.pos[r], site[r]) && (id.x & RID_FIN))
+                rxn_emit(d, L, me.x & RID_PID, id.x & RID_PID);
+            }
+        });
+    if (P.dbg_stage == 2) return;
+    const uint32_t np = min(T.npair, (uint32_t)PCAP);
+    PairBuf B;
+    B.n = 0;
+    for (uint32_t p = threadIdx.x; p < np; p += blockDim.x) {
+      const uint32_t e = T.pair[p];
+      if (e == PAIR_NONE) continue;
+      const int il = e & 0xffff, nl = e >> 16;
+      const int2 me = T.id[il], id = T.id[nl];
+      if (!(rxn_pair(NA, me, T.pos[il], site[il], id, T.pos[nl], site[nl]) && (id.x & RID_FIN))) continue;
+      const int2 v = make_int2(me.x & RID_PID, id.x & RID_PID);
+      if (B.n < 4) pair_push(B, v);
+      else rxn_emit(d, L, v.x, v.y);
     }
+    pair_flush(B, L, &d.ctl->n_pairs, d.pairs, d.cap_pairs, &d.ctl->err, [](int2 v) { return v; });
+    if (P.dbg_stage == 3) return;
     wg_flush(L, &d.ctl->n_pairs, d.pairs, d.cap_pairs, &d.ctl->err);
     return;
   }
   for (int c = threadIdx.x; c < P.tile * P.tile; c += blockDim.x) {
     int x = tx * P.tile + c % P.tile, y = ty * P.tile + c / P.tile;
     if (x >= P.ncx || y >= P.ncy) continue;
-    int r0[3], r1[3];
-    cell_ranges(P, d, x, y, r0, r1);
-    int s0 = d.cell_start[y * P.ncx + x], s1 = d.cell_start[y * P.ncx + x + 1];
+    int ra[3], sa[3], rb[3], sb[3];
+    cell_ranges(P, d, x, y, 0, ra, sa);
+    cell_ranges(P, d, x, y, 1, rb, sb);
+    int s0 = d.cell_start[cell_index(P, x, y, 0)], s1 = d.cell_start[cell_index(P, x + 1, y, 0)];
     for (int r = s0; r < s1; ++r) {
       int2 me = d.rec[r].id;
-      if ((me.x & RID_PID) >= NA || ((me.x & RID_ST2) && (me.x & RID_ST3)) || !record_final(d, me, step)) continue;
-      rxn_scan_glb(P, d, L, r0, r1, me, d.rec[r].pos, d.rec[r].site, step);
+      if (((me.x & RID_ST2) && (me.x & RID_ST3)) || !record_final(d, me, step)) continue;
+      rxn_scan_glb(P, d, L, ra, sa, me, d.rec[r].pos, d.rec[r].site, step);
+      rxn_scan_glb(P, d, L, rb, sb, me, d.rec[r].pos, d.rec[r].site, step);
     }
   }
   wg_flush(L, &d.ctl->n_pairs, d.pairs, d.cap_pairs, &d.ctl->err);
