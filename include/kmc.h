@@ -121,6 +121,15 @@ int kmc_init_random(kmc_sim* s);
 int kmc_load_cpt(kmc_sim* s, const char* path);
 int kmc_write_cpt(kmc_sim* s, const char* path);
 
+/* Exact checkpoint: the full-precision state, counters,
+ * step, seed and replica in a binary file (KMCSTAT1 layout, FNV-1a trailer).
+ * With the keyed random streams a load continues the trajectory bit for bit;
+ * a file of another size, seed or replica is refused (KMC_ERR_ARG), a corrupt
+ * one gives KMC_ERR_FORMAT.  position.cpt (3 decimals) cannot do this
+ * (main.cpp:2208-2209). */
+int kmc_save_state(kmc_sim* s, const char* path);
+int kmc_load_state(kmc_sim* s, const char* path);
+
 /* Copy the state in / out of the device (host buffers sized as above). */
 int kmc_set_state(kmc_sim* s, const kmc_state_view* v);
 int kmc_get_state(kmc_sim* s, kmc_state_view* v);
@@ -163,6 +172,8 @@ const char* kmc_host_last_error(void);
 int kmc_host_load_cpt(const kmc_params* p, const char* path, kmc_state_view* v);
 int kmc_host_write_cpt(const kmc_params* p, const kmc_state_view* v, const char* path);
 int kmc_host_init_random(const kmc_params* p, kmc_state_view* v);
+int kmc_host_save_state(const kmc_params* p, const kmc_state_view* v, const char* path);
+int kmc_host_load_state(const kmc_params* p, const char* path, kmc_state_view* v);
 /* parameter.log (main.cpp:178-205), test.gro frame (2258-2287, appended),
  * cluster.log block (2291-2305, appended) */
 int kmc_host_write_parameter_log(const kmc_params* p, const char* path);

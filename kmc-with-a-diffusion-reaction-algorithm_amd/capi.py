@@ -27,6 +27,8 @@ ERRORS = {
     -8: "KMC_ERR_GEOMETRY",
     -9: "KMC_ERR_NODEVICE",
 }
+# KMC_ERR_* as module constants (ERR_ARG = -1, ...)
+globals().update({name[4:]: code for code, name in ERRORS.items()})
 
 
 class Params(C.Structure):

@@ -464,6 +464,28 @@ int kmc_write_cpt(kmc_sim* s, const char* path) {
   return kmch_host::write_cpt(&s->p, &v, path, &s->err);
 }
 
+int kmc_save_state(kmc_sim* s, const char* path) {
+  if (!s || !path) return KMC_ERR_ARG;
+  const int NA = s->p.n_a, NB = s->p.n_b;
+  std::vector<double> ra((size_t)48 * NA + 1), rb((size_t)24 * NB + 1);
+  std::vector<int32_t> ai((size_t)5 * NA + 1), bi((size_t)8 * NB + 1);
+  kmc_state_view v{ra.data(), rb.data(), ai.data(), bi.data(), {0, 0, 0, 0, 0}, 0, 0};
+  int rc = kmc_get_state(s, &v);
+  if (rc != KMC_OK) return rc;
+  return kmch_host::save_state(&s->p, &v, path, &s->err);
+}
+
+int kmc_load_state(kmc_sim* s, const char* path) {
+  if (!s || !path) return KMC_ERR_ARG;
+  const int NA = s->p.n_a, NB = s->p.n_b;
+  std::vector<double> ra((size_t)48 * NA + 1), rb((size_t)24 * NB + 1);
+  std::vector<int32_t> ai((size_t)5 * NA + 1), bi((size_t)8 * NB + 1);
+  kmc_state_view v{ra.data(), rb.data(), ai.data(), bi.data(), {0, 0, 0, 0, 0}, 0, 0};
+  int rc = kmch_host::load_state(&s->p, path, &v, &s->err);
+  if (rc != KMC_OK) return rc;
+  return kmc_set_state(s, &v);
+}
+
 // accumulate the event pairs of ring slot `slot` (already complete or waited on)
 static void harvest(kmc_sim* s, int slot) {
   for (int k = 0; k < KI_N; ++k) {

@@ -9,6 +9,8 @@ int load_cpt(const kmc_params* p, const char* path, kmc_state_view* v, std::stri
 int write_cpt(const kmc_params* p, const kmc_state_view* v, const char* path, std::string* err);
 int validate(const kmc_params* p, const kmc_state_view* v, std::string* err);
 int init_random(const kmc_params* p, kmc_state_view* v, std::string* err);
+int save_state(const kmc_params* p, const kmc_state_view* v, const char* path, std::string* err);
+int load_state(const kmc_params* p, const char* path, kmc_state_view* v, std::string* err);
 void derived_counts(const kmc_params* p, const kmc_state_view* v, int* rl, int* mono, int* cis);
 }  // namespace kmch_host
 
@@ -18,6 +20,8 @@ const char* kmc_host_last_error(void);
 int kmc_host_load_cpt(const kmc_params* p, const char* path, kmc_state_view* v);
 int kmc_host_write_cpt(const kmc_params* p, const kmc_state_view* v, const char* path);
 int kmc_host_init_random(const kmc_params* p, kmc_state_view* v);
+int kmc_host_save_state(const kmc_params* p, const kmc_state_view* v, const char* path);
+int kmc_host_load_state(const kmc_params* p, const char* path, kmc_state_view* v);
 int kmc_host_validate(const kmc_params* p, const kmc_state_view* v);
 int kmc_host_math(int op, const double* x, const double* y, double* out, int64_t n);
 }

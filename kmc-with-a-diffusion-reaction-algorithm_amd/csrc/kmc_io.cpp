@@ -405,6 +405,108 @@ int init_random(const kmc_params* p, kmc_state_view* v, std::string* err) {
   return KMC_OK;
 }
 
+// ---------------------------------------------------------------- exact checkpoint
+// Layout (little-endian): "KMCSTAT1", u32 version, i32 n_a, i32 n_b,
+// u32 replica, u64 seed, i64 step, i32 counters[5], i32 reserved, then the
+// view's arrays in their SoA layout (ra, rb as f64; a_int, b_int as i32), then
+// an FNV-1a-64 of every preceding byte.
+namespace {
+const char kStateMagic[8] = {'K', 'M', 'C', 'S', 'T', 'A', 'T', '1'};
+struct StateHeader {
+  char magic[8];
+  uint32_t version;
+  int32_t n_a, n_b;
+  uint32_t replica;
+  uint64_t seed;
+  int64_t step;
+  int32_t counters[5];
+  int32_t reserved;
+};
+static_assert(sizeof(StateHeader) == 64, "state header layout");
+
+struct Fnv {
+  uint64_t h = 1469598103934665603ull;
+  void add(const void* p, size_t n) {
+    const unsigned char* b = (const unsigned char*)p;
+    for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
+  }
+};
+}  // namespace
+
+int save_state(const kmc_params* p, const kmc_state_view* v, const char* path, std::string* err) {
+  const size_t NA = (size_t)p->n_a, NB = (size_t)p->n_b;
+  StateHeader hd;
+  std::memset(&hd, 0, sizeof hd);
+  std::memcpy(hd.magic, kStateMagic, 8);
+  hd.version = 1;
+  hd.n_a = p->n_a;
+  hd.n_b = p->n_b;
+  hd.replica = p->replica;
+  hd.seed = p->seed;
+  hd.step = v->step;
+  for (int k = 0; k < 5; ++k) hd.counters[k] = v->counters[k];
+  FILE* f = fopen(path, "wb");
+  if (!f) {
+    *err = std::string("cannot write ") + path;
+    return KMC_ERR_IO;
+  }
+  Fnv h;
+  auto put = [&](const void* d, size_t n) {
+    h.add(d, n);
+    return fwrite(d, 1, n, f) == n;
+  };
+  bool ok = put(&hd, sizeof hd) && put(v->ra, sizeof(double) * 48 * NA) && put(v->rb, sizeof(double) * 24 * NB) &&
+            put(v->a_int, sizeof(int32_t) * 5 * NA) && put(v->b_int, sizeof(int32_t) * 8 * NB);
+  uint64_t tr = h.h;
+  ok = ok && fwrite(&tr, 1, sizeof tr, f) == sizeof tr;
+  ok = (fclose(f) == 0) && ok;
+  if (!ok) {
+    *err = std::string("write failed: ") + path;
+    return KMC_ERR_IO;
+  }
+  return KMC_OK;
+}
+
+int load_state(const kmc_params* p, const char* path, kmc_state_view* v, std::string* err) {
+  const size_t NA = (size_t)p->n_a, NB = (size_t)p->n_b;
+  FILE* f = fopen(path, "rb");
+  if (!f) {
+    *err = std::string("cannot open ") + path;
+    return KMC_ERR_IO;
+  }
+  Fnv h;
+  auto get = [&](void* d, size_t n) {
+    if (fread(d, 1, n, f) != n) return false;
+    h.add(d, n);
+    return true;
+  };
+  StateHeader hd;
+  int rc = KMC_OK;
+  if (!get(&hd, sizeof hd) || std::memcmp(hd.magic, kStateMagic, 8) != 0 || hd.version != 1) {
+    *err = std::string("not a KMCSTAT1 file: ") + path;
+    rc = KMC_ERR_FORMAT;
+  } else if (hd.n_a != p->n_a || hd.n_b != p->n_b || hd.seed != p->seed || hd.replica != p->replica) {
+    *err = "state file is of another trajectory (n_a, n_b, seed or replica differ)";
+    rc = KMC_ERR_ARG;
+  } else if (!get(v->ra, sizeof(double) * 48 * NA) || !get(v->rb, sizeof(double) * 24 * NB) ||
+             !get(v->a_int, sizeof(int32_t) * 5 * NA) || !get(v->b_int, sizeof(int32_t) * 8 * NB)) {
+    *err = std::string("truncated state file: ") + path;
+    rc = KMC_ERR_FORMAT;
+  } else {
+    uint64_t tr = 0, want = h.h;
+    if (fread(&tr, 1, sizeof tr, f) != sizeof tr || tr != want) {
+      *err = std::string("state file checksum mismatch: ") + path;
+      rc = KMC_ERR_FORMAT;
+    }
+  }
+  fclose(f);
+  if (rc != KMC_OK) return rc;
+  v->step = hd.step;
+  for (int k = 0; k < 5; ++k) v->counters[k] = hd.counters[k];
+  v->reserved = 0;
+  return validate(p, v, err);
+}
+
 }  // namespace kmch_host
 
 // ------------------------------------------------------------------ C ABI (host-only part)
@@ -530,6 +632,12 @@ int kmc_host_write_cpt(const kmc_params* p, const kmc_state_view* v, const char*
   return kmch_host::write_cpt(p, v, path, &g_host_err);
 }
 int kmc_host_init_random(const kmc_params* p, kmc_state_view* v) { return kmch_host::init_random(p, v, &g_host_err); }
+int kmc_host_save_state(const kmc_params* p, const kmc_state_view* v, const char* path) {
+  return kmch_host::save_state(p, v, path, &g_host_err);
+}
+int kmc_host_load_state(const kmc_params* p, const char* path, kmc_state_view* v) {
+  return kmch_host::load_state(p, path, v, &g_host_err);
+}
 int kmc_host_validate(const kmc_params* p, const kmc_state_view* v) { return kmch_host::validate(p, v, &g_host_err); }
 
 int kmc_host_math(int op, const double* x, const double* y, double* out, int64_t n) {

@@ -14,6 +14,9 @@
 //   kmc_run [--n-a 150] [--n-b 50] [--steps 20000000] [--box 5773 5773 1000]
 //           [--out-interval 5000] [--seed 1] [--replica 0] [--device 0]
 //           [--set name=value ...]   (any kmc_params field, e.g. ass_rate=0.04)
+//           [--state FILE]   exact checkpoint (include/kmc.h, KMCSTAT1): resumed
+//                            from when it exists (instead of position.cpt) and
+//                            rewritten with position.cpt every out_interval
 #include <sys/stat.h>
 
 #include <cstdio>
@@ -66,6 +69,7 @@ int main(int argc, char** argv) {
   kmc_params p;
   kmc_params_default(&p);
   int device = 0;
+  std::string state_path;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto next = [&]() -> std::string {
@@ -86,6 +90,7 @@ int main(int argc, char** argv) {
     else if (a == "--seed") p.seed = strtoull(next().c_str(), nullptr, 10);
     else if (a == "--replica") p.replica = (uint32_t)atoi(next().c_str());
     else if (a == "--device") device = atoi(next().c_str());
+    else if (a == "--state") state_path = next();
     else if (a == "--set") {
       std::string kv = next();
       size_t eq = kv.find('=');
@@ -105,7 +110,11 @@ int main(int argc, char** argv) {
   kmc_sim* s = nullptr;
   rc = kmc_create(&p, device, &s);
   if (rc) return die(nullptr, rc, "kmc_create");
-  if (exists("position.cpt")) {
+  if (!state_path.empty() && exists(state_path.c_str())) {
+    printf("STATE file is exist\n");
+    rc = kmc_load_state(s, state_path.c_str());
+    if (rc) return die(s, rc, state_path.c_str());
+  } else if (exists("position.cpt")) {
     printf("CPT file is exist\n");
     rc = kmc_load_cpt(s, "position.cpt");
     if (rc) return die(s, rc, "position.cpt");
@@ -138,6 +147,10 @@ int main(int argc, char** argv) {
     if (step % p.out_interval == 0) {
       rc = kmc_write_cpt(s, "position.cpt");
       if (rc) return die(s, rc, "position.cpt");
+      if (!state_path.empty()) {
+        rc = kmc_save_state(s, state_path.c_str());
+        if (rc) return die(s, rc, state_path.c_str());
+      }
       char line[256];
       kmc_format_bond_line(&p, &obs.back(), line, sizeof line);
       FILE* f = fopen("bond.dat", "ab");

@@ -66,6 +66,10 @@ def load_library(path: Optional[str] = None):
     L.kmc_host_write_cpt.argtypes = [P(capi.Params), P(capi.StateView), C.c_char_p]
     L.kmc_host_init_random.argtypes = [P(capi.Params), P(capi.StateView)]
     L.kmc_host_validate.argtypes = [P(capi.Params), P(capi.StateView)]
+    L.kmc_host_save_state.argtypes = [P(capi.Params), P(capi.StateView), C.c_char_p]
+    L.kmc_host_load_state.argtypes = [P(capi.Params), C.c_char_p, P(capi.StateView)]
+    L.kmc_save_state.argtypes = [C.c_void_p, C.c_char_p]
+    L.kmc_load_state.argtypes = [C.c_void_p, C.c_char_p]
     L.kmc_get_clusters.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     L.kmc_host_write_parameter_log.argtypes = [P(capi.Params), C.c_char_p]
     L.kmc_host_append_gro.argtypes = [P(capi.Params), P(capi.StateView), C.c_char_p]
@@ -104,6 +108,21 @@ def host_write_cpt(params: capi.Params, hs: capi.HostState, path: str) -> None:
     """host state → position.cpt (main.cpp:2206-2244)."""
     v = hs.view()
     _host_check(load_library().kmc_host_write_cpt(C.byref(params), C.byref(v), os.fsencode(path)))
+
+
+def host_save_state(params: capi.Params, hs: capi.HostState, path: str) -> None:
+    """host state → exact binary checkpoint (KMCSTAT1, include/kmc.h)."""
+    v = hs.view()
+    _host_check(load_library().kmc_host_save_state(C.byref(params), C.byref(v), os.fsencode(path)))
+
+
+def host_load_state(params: capi.Params, path: str) -> capi.HostState:
+    """exact binary checkpoint → host state (refuses another trajectory's file)."""
+    hs = capi.HostState(params.n_a, params.n_b)
+    v = hs.view()
+    _host_check(load_library().kmc_host_load_state(C.byref(params), os.fsencode(path), C.byref(v)))
+    hs.pull(v)
+    return hs
 
 
 def host_validate(params: capi.Params, hs: capi.HostState) -> int:
@@ -200,6 +219,13 @@ class Simulation:
 
     def write_cpt(self, path: str):
         self._check(load_library().kmc_write_cpt(self._h, os.fsencode(path)))
+
+    def save_state(self, path: str):
+        """Exact checkpoint: a later load_state continues the trajectory bit for bit."""
+        self._check(load_library().kmc_save_state(self._h, os.fsencode(path)))
+
+    def load_state(self, path: str):
+        self._check(load_library().kmc_load_state(self._h, os.fsencode(path)))
 
     def set_state(self, hs: capi.HostState):
         v = hs.view()

@@ -12,6 +12,7 @@ PKG = "kmc-with-a-diffusion-reaction-algorithm_amd"  # noqa
 capi = importlib.import_module(PKG + ".capi")
 engine = importlib.import_module(PKG + ".engine")
 build = importlib.import_module(PKG + ".build")
+workloads = importlib.import_module(PKG + ".workloads")
 import oracle as O  # noqa: E402  (oracle/ is on sys.path via conftest)
 
 DENSE = dict(

@@ -76,3 +76,26 @@ def test_kmc_run_fresh_and_resume(tmp_path):
     assert (wd / "position.cpt").read_bytes() == cpt2
     assert (wd / "test.gro").read_bytes() == gro + gro2
     assert (wd / "cluster.log").read_bytes() == clu + clu2
+
+
+def test_kmc_run_exact_state_resume(tmp_path):
+    # one 2000-step run vs 1000 + 1000 steps resumed from the exact state
+    # file: the final state files are byte-identical (position.cpt alone
+    # cannot give this, main.cpp:2208-2209)
+    build.build()
+    p = params(seed=19, **DENSE)
+    one, two = tmp_path / "one", tmp_path / "two"
+    one.mkdir()
+    two.mkdir()
+    r = subprocess.run(_args(p, 2000, 1000) + ["--state", "state.kmc"], cwd=one, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run(_args(p, 1000, 1000) + ["--state", "state.kmc"], cwd=two, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run(_args(p, 2000, 1000) + ["--state", "state.kmc"], cwd=two, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert "STATE file is exist" in r.stdout
+    assert (one / "state.kmc").read_bytes() == (two / "state.kmc").read_bytes()
+    assert (one / "bond.dat").read_bytes() == (two / "bond.dat").read_bytes()

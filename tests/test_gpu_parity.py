@@ -125,6 +125,30 @@ def test_frequent_slot_resort_dense(monkeypatch):
     assert st["rl"] > 0 and st["complex"] > 0
 
 
+def test_exact_state_resume(tmp_path):
+    # save after 400 dense steps, continue; a fresh handle loaded from the
+    # file must reproduce the continuation bit for bit (and the oracle's)
+    p = params(seed=31, **DENSE)
+    o = O.Oracle(p)
+    o.init_placement()
+    sim = engine.Simulation(p)
+    sim.set_state(o.get_state())
+    sim.step(400)
+    path = str(tmp_path / "state.kmc")
+    sim.save_state(path)
+    obs_a = sim.step(400)
+    h_a = engine.state_hash(p, sim.get_state())
+    sim.close()
+    sim2 = engine.Simulation(p)
+    sim2.load_state(path)
+    assert sim2.current_step == 400
+    obs_b = sim2.step(400)
+    assert np.array_equal(obs_a, obs_b)
+    assert engine.state_hash(p, sim2.get_state()) == h_a
+    o.step(800, want_hashes=False)
+    assert o.hash() == h_a
+
+
 def test_chunked_steps_equal_single_steps():
     p = params(seed=3, **DENSE)
     o = O.Oracle(p)
@@ -147,6 +171,24 @@ def test_larger_box_cell_oracle(n_a, n_b, L, steps):
     # (proven identical to the oracle's, tests/test_host.py) and the oracle's
     # cell list keep the CPU side tractable
     p = params(n_a=n_a, n_b=n_b, seed=9, box_x=L, box_y=L, box_z=250.0, **RATES)
+    st = engine.host_init_random(p)
+    o = O.Oracle(p, nbmode=O.NB_CELLS)
+    o.set_state(st)
+    sim = engine.Simulation(p)
+    sim.set_state(st)
+    obs = sim.step(steps)
+    obs_o, _ = o.step(steps, want_hashes=False)
+    assert np.array_equal(obs, obs_o)
+    assert engine.state_hash(p, sim.get_state()) == o.hash()
+
+
+@pytest.mark.parametrize("name,steps", [("C2", 100), ("C3", 8), ("C5", 2)])
+def test_benchmark_workload_window(name, steps):
+    # the benchmark configurations themselves (C2 1e5, C3 1e6
+    # dense, C5 1e7 at 1:1) bit-exact against the keyed oracle (cell mode)
+    # over a step window from the same keyed placement
+    W = __import__("_kmc").workloads
+    p = W.params(name, seed=1)
     st = engine.host_init_random(p)
     o = O.Oracle(p, nbmode=O.NB_CELLS)
     o.set_state(st)

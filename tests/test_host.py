@@ -113,3 +113,45 @@ def test_bond_line_format():
     rec["t"], rec["bond_num_rl"], rec["bond_num_mono_cis"] = 50000.0, 38, 2
     rec["bond_num_cis"], rec["bond_num"], rec["cluster_size"], rec["protein_num_in_max_complex"] = 0, 40, 2.652, 4
     assert engine.bond_line(p, rec) == "      50000.000   38    2         0        40     2.652         4\n"
+
+
+def test_exact_state_roundtrip_and_resume_on_oracle(tmp_path):
+    # KMCSTAT1 keeps every bit; resuming the keyed oracle from it continues the
+    # trajectory exactly (the 3-decimal position.cpt cannot, main.cpp:2208)
+    p = params(seed=6, **DENSE)
+    o = O.Oracle(p)
+    o.init_placement()
+    o.step(300, want_hashes=False)
+    st = o.get_state()
+    path = str(tmp_path / "state.kmc")
+    engine.host_save_state(p, st, path)
+    back = engine.host_load_state(p, path)
+    for name in ("ra", "rb", "a_int", "b_int", "counters"):
+        assert np.array_equal(getattr(back, name), getattr(st, name)), name
+    assert back.step == st.step
+    o.step(300, want_hashes=False)
+    o2 = O.Oracle(p)
+    o2.set_state(back)
+    o2.step(300, want_hashes=False)
+    assert o2.hash() == o.hash()
+
+
+def test_exact_state_refuses_other_trajectory_and_corruption(tmp_path):
+    p = params(seed=7)
+    st = engine.host_init_random(p)
+    path = tmp_path / "state.kmc"
+    engine.host_save_state(p, st, str(path))
+    other = params(seed=8)
+    with pytest.raises(engine.KmcError) as e:
+        engine.host_load_state(other, str(path))
+    assert e.value.code == capi.ERR_ARG
+    raw = bytearray(path.read_bytes())
+    raw[200] ^= 1
+    path.write_bytes(bytes(raw))
+    with pytest.raises(engine.KmcError) as e:
+        engine.host_load_state(p, str(path))
+    assert e.value.code == capi.ERR_FORMAT
+    path.write_bytes(bytes(raw[: len(raw) // 2]))
+    with pytest.raises(engine.KmcError) as e:
+        engine.host_load_state(p, str(path))
+    assert e.value.code == capi.ERR_FORMAT
