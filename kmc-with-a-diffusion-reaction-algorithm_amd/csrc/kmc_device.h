@@ -42,14 +42,10 @@ struct Ctl {
   // per-step work-list counters
   uint32_t n_overflow;    // ligands whose BFS overflowed the register queue
   uint32_t cx_cursor;     // members[] allocation cursor
-  uint32_t n_cand;        // collision candidates (resolution pass A)
-  uint32_t n_conf;        // conflict entries (pass B)
-  uint32_t n_plist;       // units with conflict entries
   uint32_t n_pend;        // units still pending after a round (pass C)
-  uint32_t n_rej;         // units rejected this step
+  uint32_t last[8];       // previous step's work counts (diagnostics): cand conf plist rej pairs rl cisc overflow
   uint32_t n_rl;          // R–L accepting edges
   uint32_t n_cisc;        // cis candidates
-  uint32_t n_pairs;       // reaction (receptor, record) pairs
   // observables (reduced per step)
   int32_t rl, mono, cis;  // derived from state
   int32_t tot_prot, tot_clu, max_size;

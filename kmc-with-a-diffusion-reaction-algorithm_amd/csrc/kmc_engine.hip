@@ -46,6 +46,7 @@ struct kmc_sim {
   int64_t obs_cap = 0;
   Ctl* ctl_host = nullptr;
   bool poison = false;
+  bool debug_counts = false;  // KMC_DEBUG_COUNTS=1: print the last step's work counts per kmc_step chunk
   // slot order (kmc_kernels.hip §slot order): scratch of the re-sort
   int64_t resort_every = 100, since_resort = 0;
   int key_bits = 1;
@@ -226,20 +227,30 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   rc |= dalloc(s, &d.members, N);
   rc |= dalloc(s, &d.pend, N);
   rc |= dalloc(s, &d.overflow, NB);
-  rc |= dalloc(s, &d.plist, N);
   rc |= dalloc(s, &d.cell_cnt, s->ncell);
   rc |= dalloc(s, &d.cell_start, s->ncell + 1);
   rc |= dalloc(s, &d.block_sums, s->nscan_blocks);
   rc |= dalloc(s, &d.rec, (size_t)2 * N);
   // collision candidates: ~1 per proposal at the benchmark densities; every
   // pair of records for small dense systems
-  d.cap_cand = (uint32_t)std::max<uint64_t>(8ull * N, std::min<uint64_t>(4ull * N * N, 1ull << 22));
-  rc |= dalloc(s, &d.cand, d.cap_cand);
-  rc |= dalloc(s, &d.conf, d.cap_cand);
-  d.cap_pairs = pow2(std::max<uint32_t>(1u << 16, (uint32_t)N));
-  rc |= dalloc(s, &d.pairs, d.cap_pairs);
+  // sharded output lists (kmc_kernels.hip §SList): per-shard capacity is the
+  // total / NSHARD, but at least 64 Ki entries (a small dense system puts all
+  // of its entries into the few shards of its few tiles)
+  rc |= dalloc(s, &d.shard_cnt, (size_t)5 * NSHARD);
+  {
+    auto mk = [&](SList& l, uint64_t total, int which) {
+      l.cap = (uint32_t)std::max<uint64_t>((total + NSHARD - 1) / NSHARD, std::min<uint64_t>(total, 1u << 16));
+      l.cnt = d.shard_cnt + which * NSHARD;
+      return dalloc(s, &l.data, (size_t)l.cap * NSHARD);
+    };
+    const uint64_t cand = std::max<uint64_t>(N, std::min<uint64_t>(4ull * N * N, 1ull << 22));
+    rc |= mk(d.cand, cand, 0);
+    rc |= mk(d.conf, cand, 1);
+    rc |= mk(d.plist, N, 2);
+    rc |= mk(d.rej, N, 3);
+    rc |= mk(d.pairs, std::max<uint64_t>(N, 1u << 16), 4);
+  }
   rc |= dalloc(s, &d.rejtag, N);
-  rc |= dalloc(s, &d.rej, N);
   rc |= dalloc(s, &d.rank, N);
   rc |= dalloc(s, &d.obs_part, (size_t)8 * ((N + 255) / 256));
   rc |= dalloc(s, &d.rl_keys, cap);
@@ -259,6 +270,8 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   }
   const char* po = getenv("KMC_DEBUG_POISON");
   s->poison = po && *po == '1';
+  const char* dc = getenv("KMC_DEBUG_COUNTS");
+  s->debug_counts = dc && *dc == '1';
   // debug: lower the LDS tile capacity so that tiles take the global path
   const char* tc = getenv("KMC_DEBUG_TCAP");
   K.tcap = TCAP;
@@ -627,6 +640,11 @@ int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out) {
     if (s->tmask)
       for (int slot = 0; slot < TRING; ++slot) harvest(s, slot);
     s->step_done += n;
+    if (s->debug_counts) {
+      const uint32_t* l = s->ctl_host->last;
+      fprintf(stderr, "kmc step %lld: candidates %u conflicts %u pending-units %u rejected %u rxn-pairs %u rl-edges %u cis-edges %u bfs-overflow %u\n",
+              (long long)s->step_done, l[0], l[1], l[2], l[3], l[4], l[5], l[6], l[7]);
+    }
     uint32_t err = s->ctl_host->err;
     if (err) {
       char m[160];

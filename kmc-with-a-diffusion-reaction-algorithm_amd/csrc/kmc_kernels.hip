@@ -29,6 +29,17 @@
 
 namespace kmcd {
 
+// Output list with NSHARD counter shards: workgroup b appends to shard
+// b % NSHARD, which owns data[shard·cap, (shard+1)·cap).  One device-scope
+// word sustains only ≈90 atomics/µs (MI355X_MICROARCH.md, dequeue / fan-in),
+// so thousands of workgroups appending to one counter would serialise.
+#define NSHARD 32
+struct SList {
+  int2* data;
+  uint32_t* cnt;  // [NSHARD]
+  uint32_t cap;   // entries per shard
+};
+
 struct Dev {
   Beads cur, nxt;
   int32_t* a_int;  // [5][NA]  st2 st3 nei2 nei4 nei3 (nei: reference 1-based)
@@ -45,20 +56,19 @@ struct Dev {
   int32_t* members;  // [N]
   uint32_t* pend;    // [N] round tag: unit still waiting (resolution pass C)
   int32_t* overflow; // [NB]
-  int32_t* plist;    // [N] units with conflict entries
   int32_t* cell_cnt;    // [ncell]
   int32_t* cell_start;  // [ncell+1]
   int32_t* block_sums;  // [scan blocks]
   struct Rec* rec;      // [2N] cell-sorted records (old and proposed position of every protein)
-  int2* cand;           // [cap_cand] collision candidates (proposal record, other record)
-  int2* conf;           // [cap_cand] conflict entries (u, kq | isnew<<31)
-  uint32_t cap_cand;
-  int2* pairs;          // [cap_pairs] reaction candidate (receptor, record)
+  SList cand;           // collision candidates (proposal record, other record)
+  SList conf;           // conflict entries (u, kq | isnew<<31)
+  SList plist;          // units with conflict entries (u, 0)
+  SList rej;            // units rejected this step (u, 0)
+  SList pairs;          // reaction candidates (receptor, partner)
+  uint32_t* shard_cnt;  // [5][NSHARD] counters of the lists above
   uint32_t* rejtag;     // [N] step at which the slot's unit was rejected (final = old position)
-  int32_t* rej;         // [N] units (keys) rejected this step
   int2* rank;           // [N] rank of the old / proposed record within its cell
   int32_t* obs_part;    // [blocks][8] per-block observable partials
-  uint32_t cap_pairs;
   uint64_t* rl_keys;    // [cap]
   uint64_t* cis_keys;   // [cap]
   uint64_t* ent;        // [2*cap] greedy scratch
@@ -1037,26 +1047,78 @@ __device__ __forceinline__ void wg_list_init(WgList& L) {
   __syncthreads();
 }
 
-__device__ __forceinline__ void wg_emit(WgList& L, int2 v, uint32_t* gctr, int2* gout, uint32_t cap, uint32_t* err) {
+__device__ __forceinline__ int my_shard() { return blockIdx.x & (NSHARD - 1); }
+
+// wave-aggregated append of the calling lanes' entries to the workgroup's shard
+__device__ __forceinline__ void sl_push(const SList& s, int2 v, uint32_t* err) {
+  const int k = my_shard();
+  const uint32_t pos = wave_slot(&s.cnt[k]);
+  if (pos < s.cap) s.data[(size_t)k * s.cap + pos] = v;
+  else atomicOr(err, ERR_EDGES);
+}
+
+__device__ __forceinline__ uint32_t sl_total(const SList& s) {
+  uint32_t t = 0;
+  for (int k = 0; k < NSHARD; ++k) t += min(s.cnt[k], s.cap);
+  return t;
+}
+
+// entry t of the concatenated shards (t < sl_total)
+__device__ __forceinline__ int2 sl_get(const SList& s, uint32_t t) {
+  int k = 0;
+  for (; k < NSHARD - 1; ++k) {
+    const uint32_t c = min(s.cnt[k], s.cap);
+    if (t < c) break;
+    t -= c;
+  }
+  return s.data[(size_t)k * s.cap + t];
+}
+
+// Block-level view of a list: pre[k] = entries in shards < k (LDS), total in
+// pre[NSHARD]; every thread of the block calls (ends with a barrier).
+__device__ __forceinline__ uint32_t sl_prefix(const SList& s, uint32_t* pre) {
+  if (threadIdx.x < 64) {
+    const int k = threadIdx.x;
+    const uint32_t c = k < NSHARD ? min(s.cnt[k], s.cap) : 0u;
+    uint32_t inc = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      uint32_t v = __shfl_up(inc, o, 64);
+      if (k >= o) inc += v;
+    }
+    if (k < NSHARD) pre[k] = inc - c;
+    if (k == NSHARD - 1) pre[NSHARD] = inc;
+  }
+  __syncthreads();
+  return pre[NSHARD];
+}
+__device__ __forceinline__ int2 sl_at(const SList& s, const uint32_t* pre, uint32_t t) {
+  int k = 0;
+#pragma unroll
+  for (int st = NSHARD / 2; st; st >>= 1)
+    if (pre[k + st] <= t) k += st;
+  return s.data[(size_t)k * s.cap + (t - pre[k])];
+}
+
+__device__ __forceinline__ void wg_emit(WgList& L, int2 v, const SList& out, uint32_t* err) {
   uint32_t s = wave_slot(&L.n);
   if (s < EBUF) {
     L.buf[s] = v;
     return;
   }
-  uint32_t pos = wave_slot(gctr);
-  if (pos < cap) gout[pos] = v;
-  else atomicOr(err, ERR_EDGES);
+  sl_push(out, v, err);
 }
 
 // all threads of the workgroup
-__device__ __forceinline__ void wg_flush(WgList& L, uint32_t* gctr, int2* gout, uint32_t cap, uint32_t* err) {
+__device__ __forceinline__ void wg_flush(WgList& L, const SList& out, uint32_t* err) {
   __syncthreads();
   const uint32_t m = min(L.n, (uint32_t)EBUF);
-  if (threadIdx.x == 0) L.base = m ? atomicAdd(gctr, m) : 0;
+  const int k = my_shard();
+  if (threadIdx.x == 0) L.base = m ? atomicAdd(&out.cnt[k], m) : 0;
   __syncthreads();
   const uint32_t base = L.base;
   for (uint32_t t = threadIdx.x; t < m; t += blockDim.x) {
-    if (base + t < cap) gout[base + t] = L.buf[t];
+    if (base + t < out.cap) out.data[(size_t)k * out.cap + base + t] = L.buf[t];
     else atomicOr(err, ERR_EDGES);
   }
 }
@@ -1248,8 +1310,7 @@ __device__ __forceinline__ void pair_push(PairBuf& b, int2 v) {
 }
 // active lanes of a wave; entries mapped through f on the way out
 template <class F>
-__device__ __forceinline__ void pair_flush(const PairBuf& b, WgList& L, uint32_t* gctr, int2* gout, uint32_t cap,
-                                           uint32_t* err, F f) {
+__device__ __forceinline__ void pair_flush(const PairBuf& b, WgList& L, const SList& out, uint32_t* err, F f) {
   const int n = min(b.n, 4);
   const uint64_t lt = (1ull << __lane_id()) - 1ull;
   const uint64_t b0 = __ballot(n & 1), b1 = __ballot(n & 2), b2 = __ballot(n & 4);
@@ -1266,8 +1327,9 @@ __device__ __forceinline__ void pair_flush(const PairBuf& b, WgList& L, uint32_t
     if (s < EBUF) {
       L.buf[s] = v;
     } else {
-      uint32_t pos = atomicAdd(gctr, 1u);
-      if (pos < cap) gout[pos] = v;
+      const int sh = my_shard();
+      const uint32_t pos = atomicAdd(&out.cnt[sh], 1u);
+      if (pos < out.cap) out.data[(size_t)sh * out.cap + pos] = v;
       else atomicOr(err, ERR_EDGES);
     }
   }
@@ -1304,7 +1366,7 @@ __device__ __forceinline__ void cell_ranges(const KParams& P, const Dev& d, int 
 //   owner kq <  u : both (which one counts is decided by kq's fate, pass C)
 // A record passing them and the conservative prefilter is a candidate.
 __device__ __forceinline__ void col_emit(const Dev& d, WgList& L, int rs, int rg) {
-  wg_emit(L, make_int2(rs, rg), &d.ctl->n_cand, d.cand, d.cap_cand, &d.ctl->err);
+  wg_emit(L, make_int2(rs, rg), d.cand, &d.ctl->err);
 }
 
 // the fate-independent filters + prefilter for one (proposal, record) pair
@@ -1385,10 +1447,10 @@ __global__ void __launch_bounds__(256) k_col_scan(KParams P, Dev d) {
       else if (B.n < 4) pair_push(B, make_int2(il, nl));
       else col_emit(d, L, tile_global(T, il), tile_global(T, nl));
     }
-    pair_flush(B, L, &d.ctl->n_cand, d.cand, d.cap_cand, &d.ctl->err,
+    pair_flush(B, L, d.cand, &d.ctl->err,
                [&](int2 v) { return make_int2(tile_global(T, v.x), tile_global(T, v.y)); });
     if (P.dbg_stage == 3) return;
-    wg_flush(L, &d.ctl->n_cand, d.cand, d.cap_cand, &d.ctl->err);
+    wg_flush(L, d.cand, &d.ctl->err);
     return;
   }
   // dense tile: one thread per interior cell, records from global memory
@@ -1412,14 +1474,14 @@ __global__ void __launch_bounds__(256) k_col_scan(KParams P, Dev d) {
       }
     }
   }
-  wg_flush(L, &d.ctl->n_cand, d.cand, d.cap_cand, &d.ctl->err);
+  wg_flush(L, d.cand, &d.ctl->err);
 }
 
 // ---------------------------------------------------------------- 4b. exact
 // u rejected; the first to reject it lists it for the commit
 __device__ __forceinline__ void mark_rej(const Dev& d, int u, uint32_t tag) {
   uint32_t old = atomicMax(&d.ustate[u], tag | S_REJ);
-  if (old != (tag | S_REJ)) d.rej[atomicAdd(&d.ctl->n_rej, 1u)] = u;  // at most once per unit: capacity N
+  if (old != (tag | S_REJ)) sl_push(d.rej, make_int2(u, 0), &d.ctl->err);  // at most once per unit
 }
 
 // Pass B: exact fp64 overlap test of each candidate (main.cpp:640-664,
@@ -1429,10 +1491,10 @@ __device__ __forceinline__ void mark_rej(const Dev& d, int u, uint32_t tag) {
 // Unit states this step: untouched = accepted, S_PEND, S_REJ (atomicMax).
 __global__ void k_col_exact(KParams P, Dev d) {
   const uint32_t tag = (d.ctl->step & 0x3fffffffu) << 2;
-  uint32_t n = d.ctl->n_cand;
-  if (n > d.cap_cand) n = d.cap_cand;
+  __shared__ uint32_t pre[NSHARD + 1];
+  const uint32_t n = sl_prefix(d.cand, pre);
   for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
-    int2 c = d.cand[t];
+    int2 c = sl_at(d.cand, pre, t);
     int2 a = d.rec[c.x].id, b = d.rec[c.y].id;
     int m = a.x & RID_PID, u = a.y, q = b.x & RID_PID, kq = b.y;
     bool isnew = b.x < 0;
@@ -1445,14 +1507,11 @@ __global__ void k_col_exact(KParams P, Dev d) {
     }
     uint32_t old = atomicMax(&d.ustate[u], tag | S_PEND);
     if ((old & ~3u) != tag) {
-      uint32_t pos = atomicAdd(&d.ctl->n_plist, 1u);
-      d.plist[pos] = u;  // at most one entry per unit: capacity N
+      sl_push(d.plist, make_int2(u, 0), &d.ctl->err);  // at most one entry per unit
     } else if ((old & 3u) == S_REJ) {
       continue;
     }
-    uint32_t pos = atomicAdd(&d.ctl->n_conf, 1u);
-    if (pos < d.cap_cand) d.conf[pos] = make_int2(u, kq | (isnew ? (int)0x80000000 : 0));
-    else atomicOr(&d.ctl->err, ERR_EDGES);
+    sl_push(d.conf, make_int2(u, kq | (isnew ? (int)0x80000000 : 0)), &d.ctl->err);
   }
 }
 
@@ -1485,20 +1544,21 @@ __device__ __forceinline__ int conf_unit(const Dev& d, int u, uint32_t step, uin
 __global__ void k_col_round(KParams P, Dev d, int round) {
   const uint32_t step = d.ctl->step;
   const uint32_t rt = round_tag(step, round);
-  uint32_t n = d.ctl->n_conf;
-  if (n > d.cap_cand) n = d.cap_cand;
+  __shared__ uint32_t pre[NSHARD + 1];
+  const uint32_t n = sl_prefix(d.conf, pre);
   if (blockIdx.x == 0 && threadIdx.x == 0) d.ctl->n_pend = 0;
   for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x)
-    conf_entry(d, d.conf[t], step, rt);
+    conf_entry(d, sl_at(d.conf, pre, t), step, rt);
 }
 
 __global__ void k_col_units(KParams P, Dev d, int round) {
   const uint32_t step = d.ctl->step;
   const uint32_t rt = round_tag(step, round);
-  uint32_t n = d.ctl->n_plist;
+  __shared__ uint32_t pre[NSHARD + 1];
+  const uint32_t n = sl_prefix(d.plist, pre);
   int pend = 0;
   for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x)
-    pend += conf_unit(d, d.plist[t], step, rt);
+    pend += conf_unit(d, sl_at(d.plist, pre, t).x, step, rt);
   if (pend) atomicAdd(&d.ctl->n_pend, (uint32_t)pend);
 }
 
@@ -1507,16 +1567,16 @@ __global__ void __launch_bounds__(1024) k_col_tail(KParams P, Dev d, int round0)
   __shared__ uint32_t npend;
   if (d.ctl->n_pend == 0) return;
   const uint32_t step = d.ctl->step;
-  uint32_t n = d.ctl->n_conf;
-  if (n > d.cap_cand) n = d.cap_cand;
-  const uint32_t nu = d.ctl->n_plist;
+  __shared__ uint32_t pre_c[NSHARD + 1], pre_u[NSHARD + 1];
+  const uint32_t n = sl_prefix(d.conf, pre_c);
+  const uint32_t nu = sl_prefix(d.plist, pre_u);
   for (int round = round0;; ++round) {
     const uint32_t rt = round_tag(step, round);
     if (threadIdx.x == 0) npend = 0;
-    for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) conf_entry(d, d.conf[t], step, rt);
+    for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) conf_entry(d, sl_at(d.conf, pre_c, t), step, rt);
     __syncthreads();
     int pend = 0;
-    for (uint32_t t = threadIdx.x; t < nu; t += blockDim.x) pend += conf_unit(d, d.plist[t], step, rt);
+    for (uint32_t t = threadIdx.x; t < nu; t += blockDim.x) pend += conf_unit(d, sl_at(d.plist, pre_u, t).x, step, rt);
     if (pend) atomicAdd(&npend, (uint32_t)pend);
     __syncthreads();
     if (npend == 0) break;
@@ -1534,9 +1594,10 @@ __global__ void __launch_bounds__(1024) k_col_tail(KParams P, Dev d, int round0)
 __global__ void k_rej_mark(KParams P, Dev d) {
   const int NA = P.NA;
   const uint32_t step = d.ctl->step;
-  const uint32_t n = d.ctl->n_rej;
+  __shared__ uint32_t pre[NSHARD + 1];
+  const uint32_t n = sl_prefix(d.rej, pre);
   for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
-    const int sl = d.slot_of[d.rej[t]];
+    const int sl = d.slot_of[sl_at(d.rej, pre, t).x];
     const uint8_t kind = d.ukind[sl];
     if (kind == U_COMPLEX) {
       const int lb = sl - NA, off = d.cx_off[lb], cs = d.cx_size[lb];
@@ -1574,7 +1635,7 @@ __device__ __forceinline__ bool record_final(const Dev& d, int2 id, uint32_t ste
 // (receptor, partner) pairs go to the exact gates of pass 2.  Record sites and
 // final flags are staged in LDS with the tile.
 __device__ __forceinline__ void rxn_emit(const Dev& d, WgList& L, int i, int q) {
-  wg_emit(L, make_int2(i, q), &d.ctl->n_pairs, d.pairs, d.cap_pairs, &d.ctl->err);
+  wg_emit(L, make_int2(i, q), d.pairs, &d.ctl->err);
 }
 
 // prefilter of one (receptor record, final-candidate record) pair
@@ -1655,9 +1716,9 @@ __global__ void __launch_bounds__(256) k_rxn_scan_tile(KParams P, Dev d) {
       if (B.n < 4) pair_push(B, v);
       else rxn_emit(d, L, v.x, v.y);
     }
-    pair_flush(B, L, &d.ctl->n_pairs, d.pairs, d.cap_pairs, &d.ctl->err, [](int2 v) { return v; });
+    pair_flush(B, L, d.pairs, &d.ctl->err, [](int2 v) { return v; });
     if (P.dbg_stage == 3) return;
-    wg_flush(L, &d.ctl->n_pairs, d.pairs, d.cap_pairs, &d.ctl->err);
+    wg_flush(L, d.pairs, &d.ctl->err);
     return;
   }
   for (int c = threadIdx.x; c < P.tile * P.tile; c += blockDim.x) {
@@ -1674,7 +1735,7 @@ __global__ void __launch_bounds__(256) k_rxn_scan_tile(KParams P, Dev d) {
       rxn_scan_glb(P, d, L, rb, sb, me, d.rec[r].pos, d.rec[r].site, step);
     }
   }
-  wg_flush(L, &d.ctl->n_pairs, d.pairs, d.cap_pairs, &d.ctl->err);
+  wg_flush(L, d.pairs, &d.ctl->err);
 }
 
 // Reaction candidates, pass 2: exact R–L association gates (main.cpp:1880-1921)
@@ -1685,10 +1746,10 @@ __global__ void k_rxn_exact(KParams P, Dev d) {
   const int NA = P.NA, NB = P.NB;
   const uint32_t step = d.ctl->step;
   const Beads& N = d.nxt;
-  uint32_t n = d.ctl->n_pairs;
-  if (n > d.cap_pairs) n = d.cap_pairs;
+  __shared__ uint32_t pre[NSHARD + 1];
+  const uint32_t n = sl_prefix(d.pairs, pre);
   for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
-    int2 pr = d.pairs[t];
+    int2 pr = sl_at(d.pairs, pre, t);
     int i = pr.x, q = pr.y;
     if (q >= NA) {
       int lb = q - NA;
@@ -2066,10 +2127,18 @@ __global__ void __launch_bounds__(256) k_finalize(KParams P, Dev d, double time_
   // per-step counters for the next step (the former k_begin)
   c->n_overflow = 0;
   c->cx_cursor = 0;
-  c->n_cand = c->n_conf = c->n_plist = c->n_pend = c->n_rej = 0;
+  c->last[0] = sl_total(d.cand);
+  c->last[1] = sl_total(d.conf);
+  c->last[2] = sl_total(d.plist);
+  c->last[3] = sl_total(d.rej);
+  c->last[4] = sl_total(d.pairs);
+  c->last[5] = c->n_rl;
+  c->last[6] = c->n_cisc;
+  c->last[7] = c->n_overflow;
+  for (int k = 0; k < 5 * NSHARD; ++k) d.shard_cnt[k] = 0;
+  c->n_pend = 0;
   c->n_rl = 0;
   c->n_cisc = 0;
-  c->n_pairs = 0;
   c->rl = c->mono = c->cis = 0;
   c->tot_prot = c->tot_clu = c->max_size = 0;
 }
