@@ -20,13 +20,13 @@ using namespace kmcd;
 // kernel ids for per-kernel HIP-event timing (kmc_set_timing / kmc_kernel_times)
 enum KId {
   KI_CLASSIFY, KI_BFS, KI_BFS_OVF, KI_PROPOSE, KI_COMPLEX, KI_REC_COUNT, KI_SCAN, KI_REC_SCATTER,
-  KI_COL_SCAN, KI_COL_EXACT, KI_COL_ROUNDS, KI_COMMIT, KI_RXN_SCAN, KI_RXN_EXACT, KI_MATCH, KI_DISS, KI_OBSERVE,
+  KI_COL_SCAN, KI_COL_EXACT, KI_COL_ROUNDS, KI_COMMIT, KI_RXN_SCAN, KI_RXN_EXACT, KI_MATCH, KI_DISS_OBSERVE,
   KI_RESORT, KI_N
 };
 static const char* const KNAMES[KI_N] = {
     "k_classify", "k_bfs", "k_bfs_overflow", "k_propose", "k_complex", "k_rec_count", "k_scan",
     "k_rec_scatter", "k_col_scan", "k_col_exact", "k_col_rounds", "k_commit", "k_rxn_scan", "k_rxn_exact",
-    "k_match", "k_diss", "k_observe", "slot_resort"};
+    "k_match", "k_diss_observe", "slot_resort"};
 #define TRING 64  // steps of event pairs kept in flight
 
 struct kmc_sim {
@@ -55,6 +55,8 @@ struct kmc_sim {
   int32_t *a_tmp = nullptr, *b_tmp = nullptr, *id_tmp = nullptr;
   void* sort_tmp = nullptr;
   size_t sort_tmp_bytes = 0;
+  void* scan_tmp = nullptr;  // hipcub exclusive scan of the cell counts
+  size_t scan_tmp_bytes = 0;
   // per-kernel timing: a ring of TRING steps of event pairs, read back lazily
   uint64_t tmask = 0;
   std::vector<hipEvent_t> tev;  // [TRING][KI_N][2]
@@ -227,7 +229,7 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   rc |= dalloc(s, &d.members, N);
   rc |= dalloc(s, &d.pend, N);
   rc |= dalloc(s, &d.overflow, NB);
-  rc |= dalloc(s, &d.cell_cnt, s->ncell);
+  rc |= dalloc(s, &d.cell_cnt, s->ncell + 1);
   rc |= dalloc(s, &d.cell_start, s->ncell + 1);
   rc |= dalloc(s, &d.block_sums, s->nscan_blocks);
   rc |= dalloc(s, &d.rec, (size_t)2 * N);
@@ -304,6 +306,17 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
     }
     s->sort_tmp_bytes = std::max<size_t>(tb, 16);
     if (dalloc(s, (uint8_t**)&s->sort_tmp, s->sort_tmp_bytes) != KMC_OK) {
+      kmc_destroy(s);
+      return KMC_ERR_HIP;
+    }
+    tb = 0;
+    if (hipcub::DeviceScan::ExclusiveSum(nullptr, tb, s->d.cell_cnt, s->d.cell_start, s->ncell + 1, s->stream) !=
+        hipSuccess) {
+      kmc_destroy(s);
+      return KMC_ERR_HIP;
+    }
+    s->scan_tmp_bytes = std::max<size_t>(tb, 16);
+    if (dalloc(s, (uint8_t**)&s->scan_tmp, s->scan_tmp_bytes) != KMC_OK) {
       kmc_destroy(s);
       return KMC_ERR_HIP;
     }
@@ -573,9 +586,10 @@ static int launch_step(kmc_sim* s, bool re_sort) {
   if (K.NB > 0) (void)hipStreamWaitEvent(st, s->ev_join, 0);
   TIMED(KI_REC_COUNT, (k_rec_count<<<gN, T, 0, st>>>(K, d)));
   TIMED(KI_SCAN, {
-    k_scan1<<<s->nscan_blocks, SCAN_T, 0, st>>>(d.cell_cnt, d.cell_start, d.block_sums, s->ncell);
-    k_scan2<<<1, SCAN_T, 0, st>>>(d.block_sums, s->nscan_blocks, d.cell_start + s->ncell);
-    k_scan3<<<s->nscan_blocks, SCAN_T, 0, st>>>(d.cell_start, d.block_sums, s->ncell);
+    // single-pass decoupled look-back scan; cell_cnt[ncell] stays 0, so
+    // cell_start[ncell] is the record total
+    size_t tb = s->scan_tmp_bytes;
+    (void)hipcub::DeviceScan::ExclusiveSum(s->scan_tmp, tb, d.cell_cnt, d.cell_start, s->ncell + 1, st);
   });
   TIMED(KI_REC_SCATTER, (k_rec_scatter<<<gN, T, 0, st>>>(K, d)));
   const int gX = std::min(2048, (K.N + T - 1) / T);  // grid-stride kernels over device-sized lists
@@ -595,10 +609,9 @@ static int launch_step(kmc_sim* s, bool re_sort) {
     TIMED(KI_RXN_SCAN, (k_rxn_scan_tile<<<ntiles, 256, 0, st>>>(K, d)));
     TIMED(KI_RXN_EXACT, (k_rxn_exact<<<1024, T, 0, st>>>(K, d)));
     TIMED(KI_MATCH, (k_match<<<1, 1024, 0, st>>>(K, d)));
-    TIMED(KI_DISS, (k_diss<<<gA, T, 0, st>>>(K, d)));
   }
-  TIMED(KI_OBSERVE, {
-    k_observe<<<gN, T, 0, st>>>(K, d);
+  TIMED(KI_DISS_OBSERVE, {
+    k_diss_observe<<<gN, T, 0, st>>>(K, d);
     k_finalize<<<1, 256, 0, st>>>(K, d, s->p.time_step, gN);
   });
   if (s->tmask) s->tslot = (s->tslot + 1) % TRING;

@@ -929,6 +929,7 @@ __global__ void k_rec_scatter(KParams P, Dev d) {
     ref_point(d, w ? d.nxt : d.cur, p, P.NA, x, y, zl, zh);
     int c = rec_cell(P, x, y, p >= NA);
     int pos = d.cell_start[c] + (w ? rk.y : rk.x);
+    d.cell_cnt[c] = 0;  // consumed by the scan: zero for the next step
     const Beads& B = w ? d.nxt : d.cur;
     Rec rc;
     rc.pos = make_float4((float)x, (float)y, (float)zl, (float)zh);
@@ -1614,11 +1615,17 @@ __global__ void k_commit(KParams P, Dev d) {
   int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P.N) return;
   if (d.rejtag[p] != d.ctl->step) return;
-  if (p < P.NA) {
-    for (int r = 0; r < 48; ++r) d.nxt.a[(size_t)r * P.NA + p] = d.cur.a[(size_t)r * P.NA + p];
-  } else {
-    int b = p - P.NA;
-    for (int r = 0; r < 24; ++r) d.nxt.b[(size_t)r * P.NB + b] = d.cur.b[(size_t)r * P.NB + b];
+  // all loads of a row batch in flight before the stores
+  const bool a = p < P.NA;
+  const int n = a ? P.NA : P.NB, i = a ? p : p - P.NA, rows = a ? 48 : 24;
+  const double* src = a ? d.cur.a : d.cur.b;
+  double* dst = a ? d.nxt.a : d.nxt.b;
+  for (int r0 = 0; r0 < rows; r0 += 24) {
+    double v[24];
+#pragma unroll
+    for (int r = 0; r < 24; ++r) v[r] = src[(size_t)(r0 + r) * n + i];
+#pragma unroll
+    for (int r = 0; r < 24; ++r) dst[(size_t)(r0 + r) * n + i] = v[r];
   }
 }
 
@@ -1973,7 +1980,7 @@ __device__ void cis_match(const KParams& P, const Dev& d) {
 // cis dissociation, mono (main.cpp:2097-2117) and complex (2120-2141): both
 // members of a pair draw in index order, so a pair breaks iff either draw
 // succeeds; handled by the lower index
-__device__ __forceinline__ void cis_diss(const KParams& P, const Dev& d, int i, int q, bool mono, uint32_t step) {
+__device__ __forceinline__ bool cis_diss(const KParams& P, const Dev& d, int i, int q, bool mono, uint32_t step) {
   const int NA = P.NA;
   uint32_t dom = mono ? kmcr::DOM_MD : kmcr::DOM_CD;
   double pd = mono ? P.p_mdiss : P.p_cdiss;
@@ -1984,7 +1991,9 @@ __device__ __forceinline__ void cis_diss(const KParams& P, const Dev& d, int i, 
     A_ST3(d, q) = 0;
     A_NEI3(d, i) = 0;
     A_NEI3(d, q) = 0;
+    return true;
   }
+  return false;
 }
 
 // both association passes in one workgroup (the cis pass reads the R–L outcome)
@@ -1997,34 +2006,6 @@ __global__ void __launch_bounds__(1024) k_match(KParams P, Dev d) {
 // R–L dissociation draw of receptor i (bonded), main.cpp:2063-2092
 __device__ __forceinline__ bool rl_breaks(const KParams& P, const Dev& d, int i, uint32_t step) {
   return kmcr::uniform(P.key, kmcr::DOM_RLD, (uint32_t)d.id_of[i], 0, step, 0) < P.p_diss;
-}
-
-// R–L dissociation (one bond per receptor: independent), then cis
-// dissociation with the R–L outcome (st2 only goes 1 -> 0, and its final
-// value is a function of the receptor's own draw, so a partner's value read
-// before or after its own update gives the same answer)
-__global__ void k_diss(KParams P, Dev d) {
-  const int NA = P.NA, NB = P.NB;
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= NA) return;
-  const uint32_t step = d.ctl->step;
-  int st2_i = A_ST2(d, i);
-  if (st2_i == 1 && rl_breaks(P, d, i, step)) {
-    int q = A_NEI2(d, i) - 1, k = A_NEI4(d, i);
-    int lb = q - NA;
-    A_ST2(d, i) = 0;
-    B_ST(d, lb, k) = 0;
-    A_NEI2(d, i) = 0;
-    A_NEI4(d, i) = 0;
-    B_NEI(d, lb, k) = 0;
-    st2_i = 0;
-  }
-  if (A_ST3(d, i) != 1) return;
-  int q = A_NEI3(d, i) - 1;
-  if (q < i) return;
-  int st2_q = A_ST2(d, q);
-  if (st2_q == 1 && rl_breaks(P, d, q, step)) st2_q = 0;
-  cis_diss(P, d, i, q, st2_i == 0 && st2_q == 0, step);
 }
 
 // ================================================================ 7. observables
@@ -2040,18 +2021,39 @@ __device__ __forceinline__ int wave_max(int v) {
   return v;
 }
 
-__global__ void __launch_bounds__(256) k_observe(KParams P, Dev d) {
-  const int NA = P.NA;
+// Dissociations and observables, one thread per protein.  Receptor i: R–L
+// dissociation (one bond per receptor: independent), then cis dissociation of
+// its pair by the lower slot with the R–L outcome (st2 only goes 1 -> 0 and
+// its final value is a function of the receptor's own draw, so the partner's
+// value read before or after its own update gives the same answer); it then
+// counts its final bonds.  Ligand: cluster statistics of this step's BFS.
+__global__ void __launch_bounds__(256) k_diss_observe(KParams P, Dev d) {
+  const int NA = P.NA, NB = P.NB;
   __shared__ int red[4][6];
   int p = blockIdx.x * blockDim.x + threadIdx.x;
   int v[6] = {0, 0, 0, 0, 0, 0};  // rl mono cis tot_prot tot_clu max
   if (p < NA) {
-    v[0] = A_ST2(d, p);
-    if (A_ST3(d, p) == 1) {
-      int q = A_NEI3(d, p) - 1;
-      if (p < q) {
-        if (A_ST2(d, p) == 0 && A_ST2(d, q) == 0) v[1] = 1;
-        else v[2] = 1;
+    const int i = p;
+    const uint32_t step = d.ctl->step;
+    int st2_i = A_ST2(d, i);
+    if (st2_i == 1 && rl_breaks(P, d, i, step)) {
+      int q = A_NEI2(d, i) - 1, k = A_NEI4(d, i);
+      int lb = q - NA;
+      A_ST2(d, i) = 0;
+      B_ST(d, lb, k) = 0;
+      A_NEI2(d, i) = 0;
+      A_NEI4(d, i) = 0;
+      B_NEI(d, lb, k) = 0;
+      st2_i = 0;
+    }
+    v[0] = st2_i;
+    if (A_ST3(d, i) == 1) {
+      int q = A_NEI3(d, i) - 1;
+      if (i < q) {
+        int st2_q = A_ST2(d, q);
+        if (st2_q == 1 && rl_breaks(P, d, q, step)) st2_q = 0;
+        const bool mono = st2_i == 0 && st2_q == 0;
+        if (!cis_diss(P, d, i, q, mono, step)) v[mono ? 1 : 2] = 1;
       }
     }
   } else if (p < P.N) {
