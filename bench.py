@@ -39,8 +39,9 @@ def kernel_bytes(name: str, n_a: int, n_b: int):
     """Algorithmic HBM bytes per launch."""
     n = n_a + n_b
     models = {
-        # read R (16 receptor / 8 ligand beads × xyz × 8 B), write R_new, unit kind
-        "k_propose": 768 * n_a + 384 * n_b + n,
+        # read R (16 receptor / 8 ligand beads × xyz × 8 B), write R_new, unit
+        # kind; the record counts it also takes write one rank pair per protein
+        "k_propose": 768 * n_a + 384 * n_b + n + 8 * n,
         # every record once (float4 + id); candidate writes are data-dependent
         "k_col_scan": 2 * n * 24,
         # old + new reference points (x, y, zlo, zhi) + receptor site, record

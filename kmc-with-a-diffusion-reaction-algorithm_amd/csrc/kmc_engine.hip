@@ -584,7 +584,6 @@ static int launch_step(kmc_sim* s, bool re_sort) {
   }
   TIMED(KI_PROPOSE, (k_propose<<<gN, T, 0, st>>>(K, d)));
   if (K.NB > 0) (void)hipStreamWaitEvent(st, s->ev_join, 0);
-  TIMED(KI_REC_COUNT, (k_rec_count<<<gN, T, 0, st>>>(K, d)));
   TIMED(KI_SCAN, {
     // single-pass decoupled look-back scan; cell_cnt[ncell] stays 0, so
     // cell_start[ncell] is the record total
@@ -601,10 +600,7 @@ static int launch_step(kmc_sim* s, bool re_sort) {
     k_col_units<<<gX, T, 0, st>>>(K, d, 0);
     k_col_tail<<<1, 1024, 0, st>>>(K, d, 1);
   });
-  TIMED(KI_COMMIT, {
-    k_rej_mark<<<gX, T, 0, st>>>(K, d);
-    k_commit<<<gN, T, 0, st>>>(K, d);
-  });
+  TIMED(KI_COMMIT, (k_rej_commit<<<gX, T, 0, st>>>(K, d)));
   if (K.NA > 0) {
     TIMED(KI_RXN_SCAN, (k_rxn_scan_tile<<<ntiles, 256, 0, st>>>(K, d)));
     TIMED(KI_RXN_EXACT, (k_rxn_exact<<<1024, T, 0, st>>>(K, d)));

@@ -267,6 +267,63 @@ __global__ void k_bfs_overflow(KParams P, Dev d) {
   }
 }
 
+// ---------------------------------------------------------------- record keys
+__device__ __forceinline__ void ref_point(const Dev& d, const Beads& B, int p, int NA, double& x, double& y,
+                                          double& zlo, double& zhi) {
+  if (p < NA) {
+    x = B.A(p, 1, 1, 0);
+    y = B.A(p, 1, 1, 1);
+    double z1 = B.A(p, 1, 1, 2), z2 = B.A(p, 2, 1, 2), z3 = B.A(p, 3, 1, 2), z4 = B.A(p, 4, 1, 2);
+    zlo = fmin(fmin(z1, z2), fmin(z3, z4));  // the axis span of the four domains
+    zhi = fmax(fmax(z1, z2), fmax(z3, z4));
+  } else {
+    x = B.B(p - NA, 1, 1, 0);
+    y = B.B(p - NA, 1, 1, 1);
+    zlo = B.B(p - NA, 1, 1, 2);
+    zhi = zlo;
+  }
+}
+
+// rigid-body extent bound the 3x3 stencil relies on (DESIGN.md §cell list)
+__device__ __forceinline__ bool extent_ok(const Beads& B, int p, int NA) {
+  if (p < NA) {
+    double x0 = B.A(p, 1, 1, 0), y0 = B.A(p, 1, 1, 1);
+    for (int j = 2; j <= 4; ++j) {
+      double dx = B.A(p, j, 1, 0) - x0, dy = B.A(p, j, 1, 1) - y0;
+      if (!(dx * dx + dy * dy <= 0.09)) return false;
+    }
+    return true;
+  }
+  int b = p - NA;
+  double x0 = B.B(b, 1, 1, 0), y0 = B.B(b, 1, 1, 1);
+  for (int j = 2; j <= 4; ++j) {
+    double dx = B.B(b, j, 1, 0) - x0, dy = B.B(b, j, 1, 1) - y0;
+    if (!(dx * dx + dy * dy <= 35.0 * 35.0)) return false;
+  }
+  return true;
+}
+
+// sort key of a record: (cell row, kind, cell column), see §LDS tiles
+__device__ __forceinline__ int rec_cell(const KParams& P, double x, double y, int kind) {
+  return (cell_y(P, y) * 2 + kind) * P.ncx + cell_x(P, x);
+}
+
+
+// A protein's two records (old and proposed position) are counted into their
+// cells by the thread that wrote the proposal (k_propose / k_complex); the
+// rank within the cell is kept for the scatter.
+__device__ __forceinline__ void count_records(const KParams& P, const Dev& d, int p) {
+  double x, y, zl, zh;
+  int2 rk;
+  const int kind = p >= P.NA;
+  ref_point(d, d.cur, p, P.NA, x, y, zl, zh);
+  rk.x = atomicAdd(&d.cell_cnt[rec_cell(P, x, y, kind)], 1);
+  ref_point(d, d.nxt, p, P.NA, x, y, zl, zh);
+  rk.y = atomicAdd(&d.cell_cnt[rec_cell(P, x, y, kind)], 1);
+  d.rank[p] = rk;
+  if (!extent_ok(d.nxt, p, P.NA)) atomicOr(&d.ctl->err, ERR_GEOMETRY);
+}
+
 // ================================================================ 2. proposals
 // free receptor, main.cpp:584-635
 __device__ void propose_free_a(const KParams& P, const Dev& d, int i, uint32_t step) {
@@ -469,9 +526,18 @@ __global__ void k_propose(KParams P, Dev d) {
   const uint32_t step = d.ctl->step;
   const int NA = P.NA;
   uint8_t k = d.ukind[p];
-  if (k == U_FREE_A) propose_free_a(P, d, p, step);
-  else if (k == U_DIMER) propose_dimer(P, d, p, A_NEI3(d, p) - 1, step);
-  else if (k == U_FREE_B) propose_free_b(P, d, p - P.NA, p, step);
+  if (k == U_FREE_A) {
+    propose_free_a(P, d, p, step);
+    count_records(P, d, p);
+  } else if (k == U_DIMER) {
+    const int q = A_NEI3(d, p) - 1;
+    propose_dimer(P, d, p, q, step);
+    count_records(P, d, p);
+    count_records(P, d, q);
+  } else if (k == U_FREE_B) {
+    propose_free_b(P, d, p - P.NA, p, step);
+    count_records(P, d, p);
+  }
 }
 
 // ---------------------------------------------------------------- complexes
@@ -797,63 +863,9 @@ __global__ void k_complex(KParams P, Dev d) {
     }
   }
   if (nB > 1) multi_ligand_align(X);
+  for (int t = 0; t < csize; ++t) count_records(P, d, res[t]);
 }
 
-// ================================================================ 3. records
-__device__ __forceinline__ void ref_point(const Dev& d, const Beads& B, int p, int NA, double& x, double& y,
-                                          double& zlo, double& zhi) {
-  if (p < NA) {
-    x = B.A(p, 1, 1, 0);
-    y = B.A(p, 1, 1, 1);
-    double z1 = B.A(p, 1, 1, 2), z2 = B.A(p, 2, 1, 2), z3 = B.A(p, 3, 1, 2), z4 = B.A(p, 4, 1, 2);
-    zlo = fmin(fmin(z1, z2), fmin(z3, z4));  // the axis span of the four domains
-    zhi = fmax(fmax(z1, z2), fmax(z3, z4));
-  } else {
-    x = B.B(p - NA, 1, 1, 0);
-    y = B.B(p - NA, 1, 1, 1);
-    zlo = B.B(p - NA, 1, 1, 2);
-    zhi = zlo;
-  }
-}
-
-// rigid-body extent bound the 3x3 stencil relies on (DESIGN.md §cell list)
-__device__ __forceinline__ bool extent_ok(const Beads& B, int p, int NA) {
-  if (p < NA) {
-    double x0 = B.A(p, 1, 1, 0), y0 = B.A(p, 1, 1, 1);
-    for (int j = 2; j <= 4; ++j) {
-      double dx = B.A(p, j, 1, 0) - x0, dy = B.A(p, j, 1, 1) - y0;
-      if (!(dx * dx + dy * dy <= 0.09)) return false;
-    }
-    return true;
-  }
-  int b = p - NA;
-  double x0 = B.B(b, 1, 1, 0), y0 = B.B(b, 1, 1, 1);
-  for (int j = 2; j <= 4; ++j) {
-    double dx = B.B(b, j, 1, 0) - x0, dy = B.B(b, j, 1, 1) - y0;
-    if (!(dx * dx + dy * dy <= 35.0 * 35.0)) return false;
-  }
-  return true;
-}
-
-// sort key of a record: (cell row, kind, cell column), see §LDS tiles
-__device__ __forceinline__ int rec_cell(const KParams& P, double x, double y, int kind) {
-  return (cell_y(P, y) * 2 + kind) * P.ncx + cell_x(P, x);
-}
-
-// cell occupancy; each record's rank within its cell is kept for the scatter
-__global__ void k_rec_count(KParams P, Dev d) {
-  int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= P.N) return;
-  double x, y, zl, zh;
-  int2 rk;
-  ref_point(d, d.cur, p, P.NA, x, y, zl, zh);
-  const int kind = p >= P.NA;
-  rk.x = atomicAdd(&d.cell_cnt[rec_cell(P, x, y, kind)], 1);
-  ref_point(d, d.nxt, p, P.NA, x, y, zl, zh);
-  rk.y = atomicAdd(&d.cell_cnt[rec_cell(P, x, y, kind)], 1);
-  d.rank[p] = rk;
-  if (!extent_ok(d.nxt, p, P.NA)) atomicOr(&d.ctl->err, ERR_GEOMETRY);
-}
 
 // exclusive scan of cell_cnt[0..n) into cell_start[0..n]; 3 kernels
 #define SCAN_T 1024
@@ -928,8 +940,13 @@ __global__ void k_rec_scatter(KParams P, Dev d) {
     double x, y, zl, zh;
     ref_point(d, w ? d.nxt : d.cur, p, P.NA, x, y, zl, zh);
     int c = rec_cell(P, x, y, p >= NA);
-    int pos = d.cell_start[c] + (w ? rk.y : rk.x);
+    const int r = w ? rk.y : rk.x;
+    int pos = d.cell_start[c] + r;
     d.cell_cnt[c] = 0;  // consumed by the scan: zero for the next step
+    if (r < 0 || pos >= d.cell_start[c + 1]) {  // a protein no unit counted: inconsistent bond graph
+      atomicOr(&d.ctl->err, ERR_RESOLVE);
+      continue;
+    }
     const Beads& B = w ? d.nxt : d.cur;
     Rec rc;
     rc.pos = make_float4((float)x, (float)y, (float)zl, (float)zh);
@@ -1592,40 +1609,34 @@ __global__ void __launch_bounds__(1024) k_col_tail(KParams P, Dev d, int round0)
 // ================================================================ 5. commit
 // The members of every rejected unit get this step's reject tag (their final
 // position is the old one); untouched units were accepted.
-__global__ void k_rej_mark(KParams P, Dev d) {
+__device__ __forceinline__ void rej_member(const KParams& P, const Dev& d, int m, uint32_t step, int lane) {
+  if (lane == 0) d.rejtag[m] = step;
+  const bool a = m < P.NA;
+  const int n = a ? P.NA : P.NB, i = a ? m : m - P.NA, rows = a ? 48 : 24;
+  const double* src = a ? d.cur.a : d.cur.b;
+  double* dst = a ? d.nxt.a : d.nxt.b;
+  if (lane < rows) dst[(size_t)lane * n + i] = src[(size_t)lane * n + i];  // R_new = R
+}
+
+// one wave per rejected unit: its members get this step's reject tag (their
+// final position is the old one) and copy R -> R_new, one bead row per lane
+__global__ void k_rej_commit(KParams P, Dev d) {
   const int NA = P.NA;
   const uint32_t step = d.ctl->step;
   __shared__ uint32_t pre[NSHARD + 1];
   const uint32_t n = sl_prefix(d.rej, pre);
-  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t w0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+  for (uint32_t t = w0; t < n; t += nw) {
     const int sl = d.slot_of[sl_at(d.rej, pre, t).x];
     const uint8_t kind = d.ukind[sl];
     if (kind == U_COMPLEX) {
       const int lb = sl - NA, off = d.cx_off[lb], cs = d.cx_size[lb];
-      for (int k = 0; k < cs; ++k) d.rejtag[d.members[off + k]] = step;
+      for (int k = 0; k < cs; ++k) rej_member(P, d, d.members[off + k], step, lane);
     } else {
-      d.rejtag[sl] = step;
-      if (kind == U_DIMER) d.rejtag[A_NEI3(d, sl) - 1] = step;
+      rej_member(P, d, sl, step, lane);
+      if (kind == U_DIMER) rej_member(P, d, A_NEI3(d, sl) - 1, step, lane);
     }
-  }
-}
-
-// rejected proteins: R_new = R
-__global__ void k_commit(KParams P, Dev d) {
-  int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= P.N) return;
-  if (d.rejtag[p] != d.ctl->step) return;
-  // all loads of a row batch in flight before the stores
-  const bool a = p < P.NA;
-  const int n = a ? P.NA : P.NB, i = a ? p : p - P.NA, rows = a ? 48 : 24;
-  const double* src = a ? d.cur.a : d.cur.b;
-  double* dst = a ? d.nxt.a : d.nxt.b;
-  for (int r0 = 0; r0 < rows; r0 += 24) {
-    double v[24];
-#pragma unroll
-    for (int r = 0; r < 24; ++r) v[r] = src[(size_t)(r0 + r) * n + i];
-#pragma unroll
-    for (int r = 0; r < 24; ++r) dst[(size_t)(r0 + r) * n + i] = v[r];
   }
 }
 
