@@ -142,12 +142,15 @@ int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out);
 int64_t kmc_current_step(const kmc_sim* s);
 
 /* Per-kernel device time, measured with HIP events on the handle's stream:
- * kmc_set_timing(s, mask) brackets every launch of the kernels whose id bit
- * is set (ids: kmc_kernel_name(0..n-1); 0 disables and resets), and
- * kmc_kernel_times returns the accumulated milliseconds and launch counts
- * since; both return the number of kernel ids.  Used by bench.py for the
- * roofline of the dominant kernel. */
+ * kmc_set_timing(s, mask) brackets the launches of the kernels whose id bit
+ * is set (ids: kmc_kernel_name(0..n-1); 0 disables and resets; returns 0),
+ * kmc_set_timing_period(s, every) brackets them only in every `every`-th step
+ * (default 1: every step; an event pair costs a few microseconds of queue
+ * time), and kmc_kernel_times returns the accumulated milliseconds and
+ * launch counts since set_timing (returns the number of kernel ids).  Used
+ * by bench.py for the roofline of the dominant kernel. */
 int kmc_set_timing(kmc_sim* s, uint64_t kernel_mask);
+int kmc_set_timing_period(kmc_sim* s, int32_t every);
 int kmc_kernel_times(const kmc_sim* s, double* total_ms, int64_t* launches, int32_t n);
 const char* kmc_kernel_name(int32_t id);
 

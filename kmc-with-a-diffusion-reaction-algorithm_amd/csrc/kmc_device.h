@@ -30,6 +30,7 @@ struct KParams {
   kmcr::Key key;
   int tcap;  // LDS tile record capacity (<= TCAP; lowered only to test the global path)
   int tile;  // cells per tile side of the LDS scans (<= TILE_MAX)
+  int cx_blocks;  // workgroups of k_complex (one wave per complex)
   int dbg_stage;  // debug timing only: stop the tile scans after stage 1 (load) / 2 (items); 0 = off
 };
 
@@ -43,12 +44,11 @@ struct Ctl {
   uint32_t n_overflow;    // ligands whose BFS overflowed the register queue
   uint32_t cx_cursor;     // members[] allocation cursor
   uint32_t n_pend;        // units still pending after a round (pass C)
+  uint32_t n_cx;          // complexes registered by the BFS this step
   uint32_t last[8];       // previous step's work counts (diagnostics): cand conf plist rej pairs rl cisc overflow
   uint32_t n_rl;          // R–L accepting edges
   uint32_t n_cisc;        // cis candidates
-  // observables (reduced per step)
-  int32_t rl, mono, cis;  // derived from state
-  int32_t tot_prot, tot_clu, max_size;
+  // observable bookkeeping (the per-step counts are reduced by k_finalize)
   int32_t off_bond, off_rl, off_cis, off_mono;  // counters − derived at load
   int32_t maxc;                                 // protein_num_in_Max_Complex
   int32_t pad2;

@@ -35,8 +35,6 @@ struct kmc_sim {
   Dev d;
   int device = 0;
   hipStream_t stream = nullptr;
-  hipStream_t side = nullptr;          // k_complex runs here, overlapping k_propose
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int64_t step_done = 0;
   std::string err;
   int ncell = 0, nscan_blocks = 0;
@@ -59,6 +57,9 @@ struct kmc_sim {
   size_t scan_tmp_bytes = 0;
   // per-kernel timing: a ring of TRING steps of event pairs, read back lazily
   uint64_t tmask = 0;
+  int32_t tperiod = 1;    // bracket only every tperiod-th step
+  int64_t tcount = 0;     // steps launched since set_timing
+  bool tnow = false;      // this step is bracketed
   std::vector<hipEvent_t> tev;  // [TRING][KI_N][2]
   std::vector<uint8_t> tused;   // [TRING][KI_N]
   int tslot = 0;
@@ -136,10 +137,7 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
     delete s;
     return KMC_ERR_NODEVICE;
   }
-  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
     kmc_destroy(s);
     return KMC_ERR_HIP;
   }
@@ -229,6 +227,7 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   rc |= dalloc(s, &d.members, N);
   rc |= dalloc(s, &d.pend, N);
   rc |= dalloc(s, &d.overflow, NB);
+  rc |= dalloc(s, &d.cx_list, NB);
   rc |= dalloc(s, &d.cell_cnt, s->ncell + 1);
   rc |= dalloc(s, &d.cell_start, s->ncell + 1);
   rc |= dalloc(s, &d.block_sums, s->nscan_blocks);
@@ -287,6 +286,8 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
     const char* te = getenv("KMC_TILE");
     if (te && *te) t = std::max(2, std::min(TILE_MAX, atoi(te)));
     K.tile = t;
+    // k_complex waves: up to one per 4 ligands, at most 4096
+    K.cx_blocks = NB > 0 ? std::min(1024, (NB + 15) / 16) : 0;
     const char* ds = getenv("KMC_DEBUG_SCAN_STAGE");
     K.dbg_stage = ds && *ds ? atoi(ds) : 0;
   }
@@ -328,16 +329,12 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
 int kmc_destroy(kmc_sim* s) {
   if (!s) return KMC_OK;
   if (s->stream) (void)hipStreamSynchronize(s->stream);
-  if (s->side) (void)hipStreamSynchronize(s->side);
   for (void* v : s->allocs) (void)hipFree(v);
   if (s->obs_buf) (void)hipFree(s->obs_buf);
   if (s->ctl_host) (void)hipHostFree(s->ctl_host);
   for (auto& e : s->tev)
     if (e) (void)hipEventDestroy(e);
   if (s->stream) (void)hipStreamDestroy(s->stream);
-  if (s->side) (void)hipStreamDestroy(s->side);
-  if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);
-  if (s->ev_join) (void)hipEventDestroy(s->ev_join);
   delete s;
   return KMC_OK;
 }
@@ -532,10 +529,10 @@ struct Bracket {
   int k;
   hipStream_t st;
   Bracket(kmc_sim* s_, int k_, hipStream_t st_) : s(s_), k(k_), st(st_) {
-    if (s->tmask >> k & 1) (void)hipEventRecord(s->tev[2 * ((size_t)s->tslot * KI_N + k)], st);
+    if (s->tnow && (s->tmask >> k & 1)) (void)hipEventRecord(s->tev[2 * ((size_t)s->tslot * KI_N + k)], st);
   }
   ~Bracket() {
-    if (s->tmask >> k & 1) {
+    if (s->tnow && (s->tmask >> k & 1)) {
       size_t i = (size_t)s->tslot * KI_N + k;
       (void)hipEventRecord(s->tev[2 * i + 1], st);
       s->tused[i] = 1;
@@ -559,7 +556,8 @@ static int launch_step(kmc_sim* s, bool re_sort) {
   hipStream_t st = s->stream;
   const int T = 256;
   const int gN = (K.N + T - 1) / T, gA = (K.NA + T - 1) / T, gB = (K.NB + T - 1) / T;
-  if (s->tmask) harvest(s, s->tslot);  // the slot's previous use is TRING steps old
+  s->tnow = s->tmask && (s->tcount++ % s->tperiod) == 0;
+  if (s->tnow) harvest(s, s->tslot);  // the slot's previous use is TRING bracketed steps old
   if (re_sort) {
     int rc;
     TIMED(KI_RESORT, rc = resort(s));
@@ -573,17 +571,10 @@ static int launch_step(kmc_sim* s, bool re_sort) {
   TIMED(KI_CLASSIFY, (k_classify<<<gN, T, 0, st>>>(K, d)));
   if (K.NB > 0) {
     TIMED(KI_BFS, (k_bfs<<<gB, T, 0, st>>>(K, d)));
-    TIMED(KI_BFS_OVF, (k_bfs_overflow<<<1, 64, 0, st>>>(K, d)));
   }
-  // complexes (few, latency-bound, disjoint proteins) overlap the proposals
-  if (K.NB > 0) {
-    (void)hipEventRecord(s->ev_fork, st);
-    (void)hipStreamWaitEvent(s->side, s->ev_fork, 0);
-    TIMED_ON(KI_COMPLEX, s->side, (k_complex<<<(K.NB + 63) / 64, 64, 0, s->side>>>(K, d)));
-    (void)hipEventRecord(s->ev_join, s->side);
-  }
+  // complexes (one wave each), then the free units
+  if (K.NB > 0) TIMED(KI_COMPLEX, (k_complex<<<K.cx_blocks, T, 0, st>>>(K, d)));
   TIMED(KI_PROPOSE, (k_propose<<<gN, T, 0, st>>>(K, d)));
-  if (K.NB > 0) (void)hipStreamWaitEvent(st, s->ev_join, 0);
   TIMED(KI_SCAN, {
     // single-pass decoupled look-back scan; cell_cnt[ncell] stays 0, so
     // cell_start[ncell] is the record total
@@ -610,7 +601,7 @@ static int launch_step(kmc_sim* s, bool re_sort) {
     k_diss_observe<<<gN, T, 0, st>>>(K, d);
     k_finalize<<<1, 256, 0, st>>>(K, d, s->p.time_step, gN);
   });
-  if (s->tmask) s->tslot = (s->tslot + 1) % TRING;
+  if (s->tnow) s->tslot = (s->tslot + 1) % TRING;
   // R_new becomes R (main.cpp:2164-2191): swap the bead buffers
   std::swap(d.cur, d.nxt);
   return KMC_OK;
@@ -744,10 +735,17 @@ int kmc_set_timing(kmc_sim* s, uint64_t kernel_mask) {
     for (auto& e : s->tev) HIPCHK(s, hipEventCreate(&e));
   }
   s->tmask = kernel_mask;
+  s->tcount = 0;
   for (int k = 0; k < KI_N; ++k) {
     s->kms[k] = 0;
     s->kcount[k] = 0;
   }
+  return KMC_OK;
+}
+
+int kmc_set_timing_period(kmc_sim* s, int32_t every) {
+  if (!s || every < 1) return KMC_ERR_ARG;
+  s->tperiod = every;
   return KMC_OK;
 }
 

@@ -56,6 +56,7 @@ struct Dev {
   int32_t* members;  // [N]
   uint32_t* pend;    // [N] round tag: unit still waiting (resolution pass C)
   int32_t* overflow; // [NB]
+  int32_t* cx_list;  // [NB] ligand (B index) of every complex root this step
   int32_t* cell_cnt;    // [ncell]
   int32_t* cell_start;  // [ncell+1]
   int32_t* block_sums;  // [scan blocks]
@@ -182,7 +183,27 @@ __device__ __forceinline__ int nbrs(const KParams& P, const Dev& d, int x, int* 
   return n;
 }
 
-__device__ void register_complex(const KParams& P, const Dev& d, int p, const int* q, int qn, bool global_q) {
+// listed: append the root to cx_list (k_complex's work list); the overflow
+// path moves its complexes itself
+// the same neighbours in three fixed slots (-1 = none), for code that must
+// not index a local array dynamically (k_complex: no scratch)
+__device__ __forceinline__ void nbrs3(const KParams& P, const Dev& d, int x, int* y) {
+  const int NA = P.NA, NB = P.NB;
+  if (x < NA) {
+    const int a = A_NEI2(d, x), b = A_NEI3(d, x);
+    y[0] = a > 0 ? a - 1 : (b > 0 ? b - 1 : -1);
+    y[1] = a > 0 && b > 0 ? b - 1 : -1;
+    y[2] = -1;
+  } else {
+    const int lb = x - NA;
+    const int v2 = B_NEI(d, lb, 2), v3 = B_NEI(d, lb, 3), v4 = B_NEI(d, lb, 4);
+    y[0] = v2 > 0 ? v2 - 1 : -1;
+    y[1] = v3 > 0 ? v3 - 1 : -1;
+    y[2] = v4 > 0 ? v4 - 1 : -1;
+  }
+}
+
+__device__ __forceinline__ void register_complex(const KParams& P, const Dev& d, int p, const int* q, int qn, bool listed) {
   uint32_t off = atomicAdd(&d.ctl->cx_cursor, (uint32_t)qn);
   if (off + qn > (uint32_t)P.N) {
     atomicOr(&d.ctl->err, ERR_MEMBERS);
@@ -200,7 +221,7 @@ __device__ void register_complex(const KParams& P, const Dev& d, int p, const in
   d.cx_size[b] = qn;
   d.cx_nb[b] = nb;
   d.ukind[p] = U_COMPLEX;
-  (void)global_q;
+  if (listed) d.cx_list[atomicAdd(&d.ctl->n_cx, 1u)] = b;
 }
 
 __global__ void k_bfs(KParams P, Dev d) {
@@ -231,40 +252,37 @@ __global__ void k_bfs(KParams P, Dev d) {
       q[qn++] = v;
     }
   }
-  register_complex(P, d, p, q, qn, false);
+  register_complex(P, d, p, q, qn, true);
 }
 
-// Components larger than BFS_QCAP: one thread, global queue + visit tags.
-__global__ void k_bfs_overflow(KParams P, Dev d) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// Component of overflow entry o (larger than BFS_QCAP): one thread, global
+// queue + visit tags.  Returns the root's ligand index if it roots the
+// component (registered, unlisted), else -1.  Called by k_complex.
+__device__ __forceinline__ int bfs_overflow_one(const KParams& P, const Dev& d, uint32_t o) {
   const int NA = P.NA;
-  uint32_t n = d.ctl->n_overflow;
-  for (uint32_t o = 0; o < n; ++o) {
-    int p = NA + d.overflow[o];
-    const int pid = d.id_of[p];
-    uint32_t tag = (uint32_t)(++d.ctl->vtag);
-    int* q = d.bfs_queue;
-    int qn = 0, head = 0;
-    q[qn++] = p;
-    d.vtag[p] = tag;
-    bool root = true;
-    while (head < qn && root) {
-      int x = q[head++];
-      int y[3];
-      int ny = nbrs(P, d, x, y);
-      for (int e = 0; e < ny; ++e) {
-        int v = y[e];
-        if (v >= NA && d.id_of[v] < pid) {
-          root = false;
-          break;
-        }
-        if (d.vtag[v] == tag) continue;
-        d.vtag[v] = tag;
-        q[qn++] = v;
-      }
+  int p = NA + d.overflow[o];
+  const int pid = d.id_of[p];
+  uint32_t tag = (uint32_t)(++d.ctl->vtag);
+  int* q = d.bfs_queue;
+  int qn = 0, head = 0;
+  q[qn++] = p;
+  d.vtag[p] = tag;
+  while (head < qn) {
+    int x = q[head++];
+    int y[3];
+    nbrs3(P, d, x, y);
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      int v = y[e];
+      if (v < 0) continue;
+      if (v >= NA && d.id_of[v] < pid) return -1;
+      if (d.vtag[v] == tag) continue;
+      d.vtag[v] = tag;
+      q[qn++] = v;
     }
-    if (root) register_complex(P, d, p, q, qn, true);
   }
+  register_complex(P, d, p, q, qn, false);
+  return p - NA;
 }
 
 // ---------------------------------------------------------------- record keys
@@ -325,8 +343,29 @@ __device__ __forceinline__ void count_records(const KParams& P, const Dev& d, in
 }
 
 // ================================================================ 2. proposals
-// free receptor, main.cpp:584-635
+// one protein's records counted from reference points held in registers:
+// the old record's rank was taken before the move (its atomic's latency
+// overlaps the proposal), the new record's here; ext: extent bound of the
+// proposal (DESIGN.md §cell list)
+__device__ __forceinline__ void count_new(const KParams& P, const Dev& d, int p, int rk_old, double nx, double ny,
+                                          bool ext) {
+  const int rk_new = atomicAdd(&d.cell_cnt[rec_cell(P, nx, ny, p >= P.NA)], 1);
+  d.rank[p] = make_int2(rk_old, rk_new);
+  if (!ext) atomicOr(&d.ctl->err, ERR_GEOMETRY);
+}
+
+// free receptor, main.cpp:584-635.  All 48 coordinates are loaded before the
+// first store (R and R_new are distinct buffers), so a lane has every load in
+// flight at once.
 __device__ void propose_free_a(const KParams& P, const Dev& d, int i, uint32_t step) {
+  double r[4][4][3];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) r[j][k][c] = d.cur.A(i, j + 1, k + 1, c);
+  const int rk_old = atomicAdd(&d.cell_cnt[rec_cell(P, r[0][0][0], r[0][0][1], 0)], 1);
   double u0, u1, u2, u3;
   const uint32_t ri = (uint32_t)d.id_of[i];
   kmcr::uniform2(P.key, kmcr::DOM_DIFF, ri, 0, step, 0, &u0, &u1);
@@ -334,32 +373,42 @@ __device__ void propose_free_a(const KParams& P, const Dev& d, int i, uint32_t s
   double amp = P.amp_a * u0;
   double phai = u1 * 2 * P.pai;
   double dx = amp * kmcm::cos(phai), dy = amp * kmcm::sin(phai);
-  double o11x = d.cur.A(i, 1, 1, 0) + dx, o11y = d.cur.A(i, 1, 1, 1) + dy;
+  double o11x = r[0][0][0] + dx, o11y = r[0][0][1] + dy;
   double PBx = P.box_x * kmcm::round_(o11x / P.box_x);
   double PBy = P.box_y * kmcm::round_(o11y / P.box_y);
   Rot t = euler(0, 0, (2 * u2 - 1) * P.rot_a);
+  double ncx[4], ncy[4];
 #pragma unroll
-  for (int j = 1; j <= 4; ++j) {
-    double cx = (d.cur.A(i, j, 1, 0) + dx) - PBx;
-    double cy = (d.cur.A(i, j, 1, 1) + dy) - PBy;
-    double cz = d.cur.A(i, j, 1, 2);
-    d.nxt.A(i, j, 1, 0) = cx;
-    d.nxt.A(i, j, 1, 1) = cy;
-    d.nxt.A(i, j, 1, 2) = cz;
+  for (int j = 0; j < 4; ++j) {
+    double cx = (r[j][0][0] + dx) - PBx;
+    double cy = (r[j][0][1] + dy) - PBy;
+    double cz = r[j][0][2];
+    ncx[j] = cx;
+    ncy[j] = cy;
+    d.nxt.A(i, j + 1, 1, 0) = cx;
+    d.nxt.A(i, j + 1, 1, 1) = cy;
+    d.nxt.A(i, j + 1, 1, 2) = cz;
 #pragma unroll
-    for (int k = 2; k <= 4; ++k) {
-      double ox = (d.cur.A(i, j, k, 0) + dx) - PBx;
-      double oy = (d.cur.A(i, j, k, 1) + dy) - PBy;
-      double oz = d.cur.A(i, j, k, 2);
-      d.nxt.A(i, j, k, 0) = rx(t, ox, oy, oz, cx, cy, cz);
-      d.nxt.A(i, j, k, 1) = ry(t, ox, oy, oz, cx, cy, cz);
-      d.nxt.A(i, j, k, 2) = rz(t, ox, oy, oz, cx, cy, cz);
+    for (int k = 1; k < 4; ++k) {
+      double ox = (r[j][k][0] + dx) - PBx;
+      double oy = (r[j][k][1] + dy) - PBy;
+      double oz = r[j][k][2];
+      d.nxt.A(i, j + 1, k + 1, 0) = rx(t, ox, oy, oz, cx, cy, cz);
+      d.nxt.A(i, j + 1, k + 1, 1) = ry(t, ox, oy, oz, cx, cy, cz);
+      d.nxt.A(i, j + 1, k + 1, 2) = rz(t, ox, oy, oz, cx, cy, cz);
     }
   }
+  bool ext = true;
+#pragma unroll
+  for (int j = 1; j < 4; ++j) {
+    double ex = ncx[j] - ncx[0], ey = ncy[j] - ncy[0];
+    ext &= ex * ex + ey * ey <= 0.09;
+  }
+  count_new(P, d, i, rk_old, ncx[0], ncy[0], ext);
 }
 
 // snap receptor a2 onto a1's cis site (x,y of all 16 beads), main.cpp:786-798
-__device__ void snap_cis(const KParams& P, const Beads& N, int a2, int a1, double cis_cut) {
+__device__ __forceinline__ void snap_cis(const KParams& P, const Beads& N, int a2, int a1, double cis_cut) {
   const double RA = P.ra;
   double x33 = N.A(a1, 3, 3, 0), x31 = N.A(a1, 3, 1, 0);
   double y33 = N.A(a1, 3, 3, 1), y31 = N.A(a1, 3, 1, 1);
@@ -383,7 +432,7 @@ __device__ void snap_cis(const KParams& P, const Beads& N, int a2, int a1, doubl
 
 // snap receptor a onto ligand site (lb = ligand 0-based in B arrays, j),
 // main.cpp:1216-1228
-__device__ void snap_bond(const KParams& P, const Beads& N, int a, int lb, int j, double bond_cut) {
+__device__ __forceinline__ void snap_bond(const KParams& P, const Beads& N, int a, int lb, int j, double bond_cut) {
   const double RA = P.ra, RB = P.rb;
   double x2 = N.B(lb, j, 2, 0), x1 = N.B(lb, j, 1, 0);
   double y2 = N.B(lb, j, 2, 1), y1 = N.B(lb, j, 1, 1);
@@ -429,7 +478,7 @@ __device__ __forceinline__ bool bond_misaligned(const KParams& P, const Beads& N
 }
 
 // cis dimer lead i with partner q, main.cpp:682-865 (proposal part)
-__device__ void propose_dimer(const KParams& P, const Dev& d, int i, int q, uint32_t step) {
+__device__ __forceinline__ void propose_dimer(const KParams& P, const Dev& d, int i, int q, uint32_t step) {
   double u0, u1, u2, u3;
   const uint32_t ri = (uint32_t)d.id_of[i];
   kmcr::uniform2(P.key, kmcr::DOM_DIFF, ri, 0, step, 0, &u0, &u1);
@@ -470,8 +519,16 @@ __device__ void propose_dimer(const KParams& P, const Dev& d, int i, int q, uint
   if (!AreSame(dist1, dist3) || !AreSame(dist2, dist4)) snap_cis(P, d.nxt, q, i, P.cis_cut);
 }
 
-// single ligand, main.cpp:905-969
+// single ligand, main.cpp:905-969 (all 24 coordinates loaded first)
 __device__ void propose_free_b(const KParams& P, const Dev& d, int lb, int p, uint32_t step) {
+  double r[4][2][3];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) r[j][k][c] = d.cur.B(lb, j + 1, k + 1, c);
+  const int rk_old = atomicAdd(&d.cell_cnt[rec_cell(P, r[0][0][0], r[0][0][1], 1)], 1);
   double u[6];
   const uint32_t rp = (uint32_t)d.id_of[p];
   kmcr::uniform2(P.key, kmcr::DOM_DIFF, rp, 0, step, 0, &u[0], &u[1]);
@@ -484,7 +541,7 @@ __device__ void propose_free_b(const KParams& P, const Dev& d, int lb, int p, ui
   double dx = amp * sth * kmcm::cos(phai);
   double dy = amp * sth * kmcm::sin(phai);
   double dz = amp * cth;
-  double o11x = d.cur.B(lb, 1, 1, 0) + dx, o11y = d.cur.B(lb, 1, 1, 1) + dy, o11z = d.cur.B(lb, 1, 1, 2) + dz;
+  double o11x = r[0][0][0] + dx, o11y = r[0][0][1] + dy, o11z = r[0][0][2] + dz;
   double PBx = P.box_x * kmcm::round_(o11x / P.box_x);
   double PBy = P.box_y * kmcm::round_(o11y / P.box_y);
   double PBz = P.box_z * kmcm::round_(o11z / P.box_z);
@@ -495,15 +552,16 @@ __device__ void propose_free_b(const KParams& P, const Dev& d, int lb, int p, ui
   for (int j = 0; j < 4; ++j)
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-      double z = d.cur.B(lb, j + 1, k + 1, 2) + dz;
+      double z = r[j][k][2] + dz;
       if (refl) z = -z + 2 * PBz;
       oz[j][k] = z;
-      ox[j][k] = (d.cur.B(lb, j + 1, k + 1, 0) + dx) - PBx;
-      oy[j][k] = (d.cur.B(lb, j + 1, k + 1, 1) + dy) - PBy;
+      ox[j][k] = (r[j][k][0] + dx) - PBx;
+      oy[j][k] = (r[j][k][1] + dy) - PBy;
     }
   // R_new[1][1] = R_new0[1][1], then every bead (incl. [1][1] itself, which
   // updates the centre in place) rotates about R_new[1][1], main.cpp:958-968
   double cx = ox[0][0], cy = oy[0][0], cz = oz[0][0];
+  double scx[4], scy[4];  // new subunit centres [j][1] (extent bound)
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -514,13 +572,26 @@ __device__ void propose_free_b(const KParams& P, const Dev& d, int lb, int p, ui
       if (j == 0 && k == 0) cy = ny;
       double nz = rz(t, ox[j][k], oy[j][k], oz[j][k], cx, cy, cz);
       if (j == 0 && k == 0) cz = nz;
+      if (k == 0) {
+        scx[j] = nx;
+        scy[j] = ny;
+      }
       d.nxt.B(lb, j + 1, k + 1, 0) = nx;
       d.nxt.B(lb, j + 1, k + 1, 1) = ny;
       d.nxt.B(lb, j + 1, k + 1, 2) = nz;
     }
+  bool ext = true;
+#pragma unroll
+  for (int j = 1; j < 4; ++j) {
+    double ex = scx[j] - scx[0], ey = scy[j] - scy[0];
+    ext &= ex * ex + ey * ey <= 35.0 * 35.0;
+  }
+  count_new(P, d, p, rk_old, scx[0], scy[0], ext);
 }
 
-__global__ void k_propose(KParams P, Dev d) {
+// One thread per slot: free receptors, cis dimers and free ligands (the
+// complexes were moved by k_complex just before).
+__global__ void __launch_bounds__(256) k_propose(KParams P, Dev d) {
   int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P.N) return;
   const uint32_t step = d.ctl->step;
@@ -528,7 +599,6 @@ __global__ void k_propose(KParams P, Dev d) {
   uint8_t k = d.ukind[p];
   if (k == U_FREE_A) {
     propose_free_a(P, d, p, step);
-    count_records(P, d, p);
   } else if (k == U_DIMER) {
     const int q = A_NEI3(d, p) - 1;
     propose_dimer(P, d, p, q, step);
@@ -536,7 +606,6 @@ __global__ void k_propose(KParams P, Dev d) {
     count_records(P, d, q);
   } else if (k == U_FREE_B) {
     propose_free_b(P, d, p - P.NA, p, step);
-    count_records(P, d, p);
   }
 }
 
@@ -587,7 +656,7 @@ struct Cx {
   }
 };
 
-__device__ void ligand_template(double rb, double tx[5][3], double ty[5][3]) {
+__device__ __forceinline__ void ligand_template(double rb, double tx[5][3], double ty[5][3]) {
   for (int j = 0; j < 5; ++j)
     for (int k = 0; k < 3; ++k) tx[j][k] = ty[j][k] = 0;
   const double s3 = kmcm::sqrt_(3.0);
@@ -600,7 +669,7 @@ __device__ void ligand_template(double rb, double tx[5][3], double ty[5][3]) {
 }
 
 // body of lable4, main.cpp:1441-1583; returns protein_B_index (0-based) after it
-__device__ int step2_body(const Cx& X, int B, int j, int a1) {
+__device__ __forceinline__ int step2_body(const Cx& X, int B, int j, int a1) {
   const KParams& P = X.P;
   const Beads& N = X.d.nxt;
   const int NA = P.NA;
@@ -616,7 +685,9 @@ __device__ int step2_body(const Cx& X, int B, int j, int a1) {
   N.B(lb, 1, 2, 2) = N.A(a1, 3, 1, 2) + P.rb;
   double tx[5][3], ty[5][3];
   ligand_template(P.rb, tx, ty);
-  double ax1 = tx[j][1], ay1 = ty[j][1];
+  // tx[j][1], ty[j][1] (j = 2..4) without a dynamically indexed array
+  double ax1 = j == 2 ? tx[2][1] : j == 3 ? tx[3][1] : tx[4][1];
+  double ay1 = j == 2 ? ty[2][1] : j == 3 ? ty[3][1] : ty[4][1];
   double ax2 = N.A(a1, 3, 1, 0) - N.A(a1, 3, 2, 0);
   double ay2 = N.A(a1, 3, 1, 1) - N.A(a1, 3, 2, 1);
   double dot = ax1 * ax2 + ay1 * ay2;
@@ -654,7 +725,7 @@ __device__ int step2_body(const Cx& X, int B, int j, int a1) {
   return Bref - 1;
 }
 
-__device__ void multi_ligand_align(const Cx& X) {
+__device__ __forceinline__ void multi_ligand_align(const Cx& X) {
   const KParams& P = X.P;
   const Beads& N = X.d.nxt;
   const int NA = P.NA;
@@ -774,17 +845,21 @@ __device__ void multi_ligand_align(const Cx& X) {
   }
 }
 
-__global__ void k_complex(KParams P, Dev d) {
-  int lb = blockIdx.x * blockDim.x + threadIdx.x;
-  if (lb >= P.NB) return;
-  int p = P.NA + lb;
-  if (d.ukind[p] != U_COMPLEX) return;
+// One wave per complex.  The order-dependent sums (periodic shift, centre of
+// mass: BFS member order, main.cpp:1007-1067) are accumulated in member order
+// by every lane from shuffled per-member values, the rigid move is spread
+// over (member, bead) lanes, the lay-down / alignment code (sequential,
+// data-dependent, rare) runs on lane 0, and the members' records are counted
+// in parallel.  Lanes exchange bead values through global memory only after
+// a workgroup-scope fence (the wave's lanes share the CU's L1).
+__device__ __forceinline__ void complex_wave(const KParams& P, const Dev& d, int lb, int lane) {
+  const int p = P.NA + lb;
   const int NA = P.NA;
   const uint32_t step = d.ctl->step;
   Cx X{P, d, step, p, (uint32_t)d.id_of[p], d.members + d.cx_off[lb], d.cx_size[lb]};
-  int* res = X.res;
+  const int* res = X.res;
   const int csize = X.size;
-  int nB = d.cx_nb[lb], nA = csize - nB;
+  const int nB = d.cx_nb[lb], nA = csize - nB;
   // rigid move, main.cpp:974-1131
   double u0, u1, u2, u3;
   kmcr::uniform2(P.key, kmcr::DOM_DIFF, X.rootid, 0, step, 0, &u0, &u1);
@@ -792,80 +867,147 @@ __global__ void k_complex(KParams P, Dev d) {
   double amp = (nB == 1 ? P.amp_bond : 0.0) * u0;
   double phai = u1 * 2 * P.pai;
   double dx = amp * kmcm::cos(phai), dy = amp * kmcm::sin(phai);
+  // lane = (member ql of a pass of four, bead slot (j-1)*4 + (k-1)); the
+  // first pass's beads stay in registers (most complexes have <= 4 members)
+  const int ql = lane >> 4, bj = ((lane >> 2) & 3) + 1, bk = (lane & 3) + 1;
+  const int npass = (csize + 3) >> 2;
+  double c0x = 0, c0y = 0, c0z = 0;
+  bool c0 = false;
+  if (ql < csize) {
+    const int m = res[ql];
+    c0 = bk <= X.nk(m);
+    if (c0) {
+      c0x = X.R(m, bj, bk, 0);
+      c0y = X.R(m, bj, bk, 1);
+      c0z = X.R(m, bj, bk, 2);
+    }
+  }
+  // bead of this lane in pass ps: valid?, R coordinates
+  auto bead = [&](int ps, double& x, double& y, double& z) -> bool {
+    if (ps == 0) {
+      x = c0x;
+      y = c0y;
+      z = c0z;
+      return c0;
+    }
+    const int q = ps * 4 + ql;
+    if (q >= csize) return false;
+    const int m = res[q];
+    if (bk > X.nk(m)) return false;
+    x = X.R(m, bj, bk, 0);
+    y = X.R(m, bj, bk, 1);
+    z = X.R(m, bj, bk, 2);
+    return true;
+  };
+  // periodic shift from the members' [1][1] in member order (main.cpp:994-1004)
   double PBx = 0, PBy = 0;
-  for (int t = 0; t < csize; ++t) {
-    int m = res[t];
-    PBx = PBx + (X.R(m, 1, 1, 0) + dx);
-    PBy = PBy + (X.R(m, 1, 1, 1) + dy);
+  for (int ps = 0; ps < npass; ++ps) {
+    double x = 0, y = 0, z = 0;
+    bead(ps, x, y, z);
+    const double vx = x + dx, vy = y + dy;
+    const int cnt = min(4, csize - ps * 4);
+    for (int s = 0; s < cnt; ++s) {
+      PBx = PBx + __shfl(vx, s * 16, 64);
+      PBy = PBy + __shfl(vy, s * 16, 64);
+    }
   }
   PBx = P.box_x * kmcm::round_(PBx / (nA + nB) / P.box_x);
   PBy = P.box_y * kmcm::round_(PBy / (nA + nB) / P.box_y);
+  // centre of the members' [j][1] beads, member order then j (main.cpp:1007-1021)
   double cmx = 0, cmy = 0, cmz = 0;
-  for (int t = 0; t < csize; ++t) {
-    int m = res[t];
-    for (int j = 1; j <= 4; ++j) {
-      cmx = cmx + ((X.R(m, j, 1, 0) + dx) - PBx);
-      cmy = cmy + ((X.R(m, j, 1, 1) + dy) - PBy);
-      cmz = cmz + X.R(m, j, 1, 2);
-    }
+  for (int ps = 0; ps < npass; ++ps) {
+    double x = 0, y = 0, z = 0;
+    bead(ps, x, y, z);
+    const double ax = (x + dx) - PBx, ay = (y + dy) - PBy;
+    const int cnt = min(4, csize - ps * 4);
+    for (int s = 0; s < cnt; ++s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        cmx = cmx + __shfl(ax, s * 16 + j * 4, 64);
+        cmy = cmy + __shfl(ay, s * 16 + j * 4, 64);
+        cmz = cmz + __shfl(z, s * 16 + j * 4, 64);
+      }
   }
   cmx = cmx / (4 * nA + 4 * nB);
   cmy = cmy / (4 * nA + 4 * nB);
   cmz = cmz / (4 * nA + 4 * nB);
   Rot t = euler(0, 0, (2 * u2 - 1) * (nB == 1 ? P.rot_bond : 0.0));
-  int pA = -1, pB = -1;
-  for (int q = 0; q < csize; ++q) {
-    int m = res[q];
-    int nk = X.nk(m);
-    for (int j = 1; j <= 4; ++j)
-      for (int k = 1; k <= nk; ++k) {
-        double ox = (X.R(m, j, k, 0) + dx) - PBx;
-        double oy = (X.R(m, j, k, 1) + dy) - PBy;
-        double oz = X.R(m, j, k, 2);
-        X.N(m, j, k, 0) = rx(t, ox, oy, oz, cmx, cmy, cmz);
-        X.N(m, j, k, 1) = ry(t, ox, oy, oz, cmx, cmy, cmz);
-        X.N(m, j, k, 2) = rz(t, ox, oy, oz, cmx, cmy, cmz);
-      }
-    if (m < NA) pA = m;
-    else pB = m;
+  for (int ps = 0; ps < npass; ++ps) {
+    double x = 0, y = 0, z = 0;
+    if (!bead(ps, x, y, z)) continue;
+    const int m = res[ps * 4 + ql];
+    double ox = (x + dx) - PBx;
+    double oy = (y + dy) - PBy;
+    double oz = z;
+    X.N(m, bj, bk, 0) = rx(t, ox, oy, oz, cmx, cmy, cmz);
+    X.N(m, bj, bk, 1) = ry(t, ox, oy, oz, cmx, cmy, cmz);
+    X.N(m, bj, bk, 2) = rz(t, ox, oy, oz, cmx, cmy, cmz);
   }
-  const Beads& N = d.nxt;
-  if (nB == 1) {
-    int lbB = pB - NA;
-    // lay-down, main.cpp:1140-1193 (exact != test)
-    if (N.B(lbB, 1, 2, 2) != (N.B(lbB, 1, 1, 2) + P.rb)) {
-      for (int j = 1; j <= 4; ++j)
-        for (int k = 1; k <= 2; ++k) N.B(lbB, j, k, 2) = N.A(pA, 3, 1, 2);
-      N.B(lbB, 1, 2, 2) = N.A(pA, 3, 1, 2) + P.rb;
-      double angle = kmcm::atan2((N.B(lbB, 2, 1, 0) - N.B(lbB, 1, 1, 0)), (N.B(lbB, 2, 1, 1) - N.B(lbB, 1, 1, 1))) + P.pai;
-      double tx[5][3], ty[5][3];
-      ligand_template(P.rb, tx, ty);
-      double c0x = N.B(lbB, 1, 1, 0), c0y = N.B(lbB, 1, 1, 1);
-      double ca = kmcm::cos(angle), sa = kmcm::sin(angle);
-      for (int j = 1; j <= 4; ++j)
-        for (int k = 1; k <= 2; ++k) {
-          N.B(lbB, j, k, 0) = tx[j][k] * ca - ty[j][k] * sa + c0x;
-          N.B(lbB, j, k, 1) = tx[j][k] * sa + ty[j][k] * ca + c0y;
+  int pA = -1;  // last receptor in member order (the lay-down's receptor)
+  for (int base = 0; base < csize; base += 64) {
+    const int t2 = base + lane;
+    const int m = t2 < csize ? res[t2] : -1;
+    const uint64_t am = __ballot(t2 < csize && m < NA);
+    if (am) pA = __shfl(m, 63 - __clzll((long long)am), 64);
+  }
+  __threadfence_block();
+  if (lane == 0) {
+    const Beads& N = d.nxt;
+    if (nB == 1) {
+      const int lbB = lb;  // the only ligand is the root
+      // lay-down, main.cpp:1140-1193 (exact != test)
+      if (N.B(lbB, 1, 2, 2) != (N.B(lbB, 1, 1, 2) + P.rb)) {
+        for (int j = 1; j <= 4; ++j)
+          for (int k = 1; k <= 2; ++k) N.B(lbB, j, k, 2) = N.A(pA, 3, 1, 2);
+        N.B(lbB, 1, 2, 2) = N.A(pA, 3, 1, 2) + P.rb;
+        double angle = kmcm::atan2((N.B(lbB, 2, 1, 0) - N.B(lbB, 1, 1, 0)), (N.B(lbB, 2, 1, 1) - N.B(lbB, 1, 1, 1))) + P.pai;
+        double tx[5][3], ty[5][3];
+        ligand_template(P.rb, tx, ty);
+        double l0x = N.B(lbB, 1, 1, 0), l0y = N.B(lbB, 1, 1, 1);
+        double ca = kmcm::cos(angle), sa = kmcm::sin(angle);
+        for (int j = 1; j <= 4; ++j)
+          for (int k = 1; k <= 2; ++k) {
+            N.B(lbB, j, k, 0) = tx[j][k] * ca - ty[j][k] * sa + l0x;
+            N.B(lbB, j, k, 1) = tx[j][k] * sa + ty[j][k] * ca + l0y;
+          }
+      }
+      // align attached receptors, main.cpp:1196-1233
+      for (int j = 2; j <= 4; ++j) {
+        int a1ref = X.neiB(lbB, j);
+        if (a1ref != 0 && bond_misaligned(P, N, lbB, j, a1ref - 1)) snap_bond(P, N, a1ref - 1, lbB, j, P.bond_cut);
+      }
+      // align their cis partners, main.cpp:1237-1274
+      for (int j = 2; j <= 4; ++j) {
+        int a1ref = X.neiB(lbB, j);
+        if (a1ref != 0 && X.neiA3(a1ref - 1) != 0) {
+          int a1 = a1ref - 1, a2 = X.neiA3(a1) - 1;
+          if (cis_misaligned(P, N, a1, a2)) snap_cis(P, N, a2, a1, P.cis_cut);
         }
-    }
-    // align attached receptors, main.cpp:1196-1233
-    for (int j = 2; j <= 4; ++j) {
-      int a1ref = X.neiB(lbB, j);
-      if (a1ref != 0 && bond_misaligned(P, N, lbB, j, a1ref - 1)) snap_bond(P, N, a1ref - 1, lbB, j, P.bond_cut);
-    }
-    // align their cis partners, main.cpp:1237-1274
-    for (int j = 2; j <= 4; ++j) {
-      int a1ref = X.neiB(lbB, j);
-      if (a1ref != 0 && X.neiA3(a1ref - 1) != 0) {
-        int a1 = a1ref - 1, a2 = X.neiA3(a1) - 1;
-        if (cis_misaligned(P, N, a1, a2)) snap_cis(P, N, a2, a1, P.cis_cut);
       }
     }
+    if (nB > 1) multi_ligand_align(X);
   }
-  if (nB > 1) multi_ligand_align(X);
-  for (int t = 0; t < csize; ++t) count_records(P, d, res[t]);
+  __threadfence_block();
+  for (int t2 = lane; t2 < csize; t2 += 64) count_records(P, d, res[t2]);
 }
 
+// P.cx_blocks workgroups; each wave takes complexes from the BFS's root list.
+// Wave 0 first runs the BFS of the components that overflowed k_bfs's
+// register queue (rare: > BFS_QCAP members) and moves those it roots.
+__global__ void __launch_bounds__(256) k_complex(KParams P, Dev d) {
+  const int w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), nw = gridDim.x * (blockDim.x >> 6);
+  const uint32_t n = d.ctl->n_cx;
+  if (w == 0) {
+    const uint32_t no = d.ctl->n_overflow;
+    for (uint32_t o = 0; o < no; ++o) {
+      int lb = __lane_id() == 0 ? bfs_overflow_one(P, d, o) : -1;
+      lb = __shfl(lb, 0, 64);
+      __threadfence_block();
+      if (lb >= 0) complex_wave(P, d, lb, __lane_id());
+    }
+  }
+  for (uint32_t c = w; c < n; c += nw) complex_wave(P, d, d.cx_list[c], __lane_id());
+}
 
 // exclusive scan of cell_cnt[0..n) into cell_start[0..n]; 3 kernels
 #define SCAN_T 1024
@@ -2092,9 +2234,13 @@ __global__ void __launch_bounds__(256) k_diss_observe(KParams P, Dev d) {
 }
 
 // bond.dat record (main.cpp:2195-2202, 2251) and step advance; one
-// workgroup reduces the observable partials of k_observe's nblk blocks
+// workgroup reduces the observable partials of k_diss_observe's nblk blocks.
+// The list shard counters are totalled (diagnostics) and zeroed in parallel;
+// the control block is read in one batch of loads and written once.
 __global__ void __launch_bounds__(256) k_finalize(KParams P, Dev d, double time_step, int nblk) {
   __shared__ int red[4][6];
+  __shared__ uint32_t tot[5];
+  if (threadIdx.x < 5) tot[threadIdx.x] = 0;
   int v[6] = {0, 0, 0, 0, 0, 0};
   for (int b = threadIdx.x; b < nblk; b += blockDim.x) {
     const int4 lo = *(const int4*)&d.obs_part[b * 8];
@@ -2111,49 +2257,48 @@ __global__ void __launch_bounds__(256) k_finalize(KParams P, Dev d, double time_
   if ((threadIdx.x & 63) == 0)
     for (int f = 0; f < 6; ++f) red[threadIdx.x >> 6][f] = v[f];
   __syncthreads();
+  if (threadIdx.x < 5 * NSHARD) {  // lists in shard_cnt order: cand conf plist rej pairs
+    const int l = threadIdx.x / NSHARD;
+    const uint32_t cap = l == 0 ? d.cand.cap : l == 1 ? d.conf.cap : l == 2 ? d.plist.cap : l == 3 ? d.rej.cap : d.pairs.cap;
+    atomicAdd(&tot[l], min(d.shard_cnt[threadIdx.x], cap));
+    d.shard_cnt[threadIdx.x] = 0;
+  }
+  __syncthreads();
   if (threadIdx.x != 0) return;
   for (int w = 1; w < (int)(blockDim.x >> 6); ++w)
     for (int f = 0; f < 6; ++f) red[0][f] = f == 5 ? max(red[0][f], red[w][f]) : red[0][f] + red[w][f];
   Ctl* c = d.ctl;
-  c->rl = red[0][0];
-  c->mono = red[0][1];
-  c->cis = red[0][2];
-  c->tot_prot = red[0][3];
-  c->tot_clu = red[0][4];
-  c->max_size = red[0][5];
-  if (c->max_size > c->maxc) c->maxc = c->max_size;
+  const uint32_t step = c->step, obs_idx = c->obs_idx, n_rl = c->n_rl, n_cisc = c->n_cisc, n_ovf = c->n_overflow;
+  const int32_t off_rl = c->off_rl, off_mono = c->off_mono, off_cis = c->off_cis, off_bond = c->off_bond;
+  const int32_t rl = red[0][0], mono = red[0][1], cis = red[0][2], tot_prot = red[0][3], tot_clu = red[0][4];
+  const int32_t maxc = max(c->maxc, red[0][5]);
   kmc_obs_dev o;
-  o.step = (int64_t)c->step;
-  o.t = (double)(int)c->step * time_step;
-  o.rl = c->rl + c->off_rl;
-  o.mono = c->mono + c->off_mono;
-  o.cis = c->cis + c->off_cis;
-  o.bond = (c->rl + c->mono + c->cis) + c->off_bond;
-  o.cluster_size = c->tot_clu != 0 ? (double)c->tot_prot / c->tot_clu : 0.0;
-  o.maxc = c->maxc;
-  o.tot_prot = c->tot_prot;
-  o.tot_clu = c->tot_clu;
+  o.step = (int64_t)step;
+  o.t = (double)(int)step * time_step;
+  o.rl = rl + off_rl;
+  o.mono = mono + off_mono;
+  o.cis = cis + off_cis;
+  o.bond = (rl + mono + cis) + off_bond;
+  o.cluster_size = tot_clu != 0 ? (double)tot_prot / tot_clu : 0.0;
+  o.maxc = maxc;
+  o.tot_prot = tot_prot;
+  o.tot_clu = tot_clu;
   o.reserved = 0;
-  d.obs[c->obs_idx] = o;
-  c->obs_idx = c->obs_idx + 1;
-  c->step = c->step + 1;
-  // per-step counters for the next step (the former k_begin)
+  d.obs[obs_idx] = o;
+  c->maxc = maxc;
+  c->obs_idx = obs_idx + 1;
+  c->step = step + 1;
+  // per-step counters for the next step; the finished step's work counts
+  for (int k = 0; k < 5; ++k) c->last[k] = tot[k];
+  c->last[5] = n_rl;
+  c->last[6] = n_cisc;
+  c->last[7] = n_ovf;
   c->n_overflow = 0;
   c->cx_cursor = 0;
-  c->last[0] = sl_total(d.cand);
-  c->last[1] = sl_total(d.conf);
-  c->last[2] = sl_total(d.plist);
-  c->last[3] = sl_total(d.rej);
-  c->last[4] = sl_total(d.pairs);
-  c->last[5] = c->n_rl;
-  c->last[6] = c->n_cisc;
-  c->last[7] = c->n_overflow;
-  for (int k = 0; k < 5 * NSHARD; ++k) d.shard_cnt[k] = 0;
+  c->n_cx = 0;
   c->n_pend = 0;
   c->n_rl = 0;
   c->n_cisc = 0;
-  c->rl = c->mono = c->cis = 0;
-  c->tot_prot = c->tot_clu = c->max_size = 0;
 }
 
 

@@ -55,6 +55,7 @@ def load_library(path: Optional[str] = None):
     L.kmc_current_step.restype = C.c_int64
     L.kmc_current_step.argtypes = [C.c_void_p]
     L.kmc_set_timing.argtypes = [C.c_void_p, C.c_uint64]
+    L.kmc_set_timing_period.argtypes = [C.c_void_p, C.c_int32]
     L.kmc_kernel_times.argtypes = [C.c_void_p, P(C.c_double), P(C.c_int64), C.c_int32]
     L.kmc_kernel_name.restype = C.c_char_p
     L.kmc_kernel_name.argtypes = [C.c_int32]
@@ -256,13 +257,15 @@ class Simulation:
     def current_step(self) -> int:
         return int(load_library().kmc_current_step(self._h))
 
-    def set_timing(self, kernels=()):
-        """Bracket the named kernels with HIP events (empty: off)."""
+    def set_timing(self, kernels=(), every: int = 1):
+        """Bracket the named kernels with HIP events (empty: off), in every
+        `every`-th step only."""
         names = kernel_names()
         mask = 0
         for k in kernels:
             mask |= 1 << names.index(k)
         self._check(load_library().kmc_set_timing(self._h, mask))
+        self._check(load_library().kmc_set_timing_period(self._h, every))
 
     def kernel_times(self) -> dict:
         """{kernel: (total_ms, launches)} accumulated since set_timing."""
