@@ -69,7 +69,8 @@ def _build_driver(verbose: bool) -> None:
 def _build_lib(verbose: bool) -> str:
     os.makedirs(LIB_DIR, exist_ok=True)
     tmp = LIB + ".tmp"
-    cmd = [HIPCC, *FLAGS, "-o", tmp, *[os.path.join(CSRC, s) for s in SOURCES]]
+    extra = os.environ.get("KMC_EXTRA_FLAGS", "").split()  # diagnostic builds only (e.g. -DKMC_STAMPS)
+    cmd = [HIPCC, *FLAGS, *extra, "-o", tmp, *[os.path.join(CSRC, s) for s in SOURCES]]
     if verbose:
         print(" ".join(cmd))
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -53,6 +53,7 @@ struct Ctl {
   int32_t maxc;                                 // protein_num_in_Max_Complex
   int32_t pad2;
   uint64_t vtag;          // BFS tag counter for the overflow path
+  uint64_t stamps[16];    // diagnostic build (-DKMC_STAMPS) only: tile-scan phase cycles
 };
 
 enum : uint32_t {

@@ -251,7 +251,6 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
     rc |= mk(d.rej, N, 3);
     rc |= mk(d.pairs, std::max<uint64_t>(N, 1u << 16), 4);
   }
-  rc |= dalloc(s, &d.rejtag, N);
   rc |= dalloc(s, &d.rank, N);
   rc |= dalloc(s, &d.obs_part, (size_t)8 * ((N + 255) / 256));
   rc |= dalloc(s, &d.rl_keys, cap);
@@ -417,7 +416,6 @@ int kmc_set_state(kmc_sim* s, const kmc_state_view* v) {
   HIPCHK(s, hipMemcpy(d.ctl, &c, sizeof c, hipMemcpyHostToDevice));
   HIPCHK(s, hipMemset(d.ustate, 0, sizeof(uint32_t) * (size_t)(NA + NB)));
   HIPCHK(s, hipMemset(d.moved, 0, sizeof(uint32_t) * (size_t)(NA + NB)));
-  HIPCHK(s, hipMemset(d.rejtag, 0, sizeof(uint32_t) * (size_t)(NA + NB)));
   // reference order = identity slots, then the spatial sort
   k_iota<<<(NA + NB + 255) / 256, 256, 0, s->stream>>>(d.id_of, d.slot_of, NA + NB);
   rc = resort(s);
@@ -644,6 +642,13 @@ int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out) {
       const uint32_t* l = s->ctl_host->last;
       fprintf(stderr, "kmc step %lld: candidates %u conflicts %u pending-units %u rejected %u rxn-pairs %u rl-edges %u cis-edges %u bfs-overflow %u\n",
               (long long)s->step_done, l[0], l[1], l[2], l[3], l[4], l[5], l[6], l[7]);
+      const uint64_t* t = s->ctl_host->stamps;
+      if (t[0] | t[8])
+        fprintf(stderr, "kmc stamps col %llu %llu %llu %llu %llu %llu %llu %llu rxn %llu %llu %llu %llu %llu %llu %llu %llu\n",
+                (unsigned long long)t[0], (unsigned long long)t[1], (unsigned long long)t[2], (unsigned long long)t[3],
+                (unsigned long long)t[4], (unsigned long long)t[5], (unsigned long long)t[6], (unsigned long long)t[7],
+                (unsigned long long)t[8], (unsigned long long)t[9], (unsigned long long)t[10], (unsigned long long)t[11],
+                (unsigned long long)t[12], (unsigned long long)t[13], (unsigned long long)t[14], (unsigned long long)t[15]);
     }
     uint32_t err = s->ctl_host->err;
     if (err) {

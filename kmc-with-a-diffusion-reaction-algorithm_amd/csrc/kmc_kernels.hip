@@ -67,7 +67,6 @@ struct Dev {
   SList rej;            // units rejected this step (u, 0)
   SList pairs;          // reaction candidates (receptor, partner)
   uint32_t* shard_cnt;  // [5][NSHARD] counters of the lists above
-  uint32_t* rejtag;     // [N] step at which the slot's unit was rejected (final = old position)
   int2* rank;           // [N] rank of the old / proposed record within its cell
   int32_t* obs_part;    // [blocks][8] per-block observable partials
   uint64_t* rl_keys;    // [cap]
@@ -1069,6 +1068,8 @@ __global__ void k_scan3(int32_t* out, const int32_t* sums, int n) {
 }
 
 #define RID_PID 0x00ffffff
+#define RID_FIN (1 << 24)  // record holds its protein's final position (new: set by the scatter; moved to
+                           // the old record by k_rej_commit for rejected units)
 #define RID_ST3 (1 << 29)
 #define RID_ST2 (1 << 30)
 __global__ void k_rec_scatter(KParams P, Dev d) {
@@ -1092,7 +1093,7 @@ __global__ void k_rec_scatter(KParams P, Dev d) {
     const Beads& B = w ? d.nxt : d.cur;
     Rec rc;
     rc.pos = make_float4((float)x, (float)y, (float)zl, (float)zh);
-    rc.id = make_int2(p | st | (w << 31), d.owner[p]);
+    rc.id = make_int2(p | st | (w << 31) | (w ? RID_FIN : 0), d.owner[p]);
     rc.site = p < NA ? make_float2((float)B.A(p, 3, 3, 0), (float)B.A(p, 3, 3, 1)) : make_float2(0.f, 0.f);
     d.rec[pos] = rc;  // one 32-byte store
   }
@@ -1183,7 +1184,7 @@ __device__ __forceinline__ bool prefilter(bool mA, float mx, float my, float mzl
 // (slots handed out per wave: one LDS atomic per emitting wave-instruction),
 // and one global atomicAdd per workgroup reserves the output range.  Entries
 // beyond the LDS buffer go straight to global memory.
-#define EBUF 256
+#define EBUF 128
 struct WgList {
   int2 buf[EBUF];
   uint32_t n;
@@ -1283,6 +1284,34 @@ __device__ __forceinline__ void wg_flush(WgList& L, const SList& out, uint32_t* 
   }
 }
 
+// ---------------------------------------------------------------- stamps
+// Diagnostic build only (-DKMC_STAMPS): thread 0 of each workgroup adds the
+// cycles since its previous stamp to ctl->stamps[base + i] (phase shares of
+// the tile scans; kmc_step prints them with KMC_DEBUG_COUNTS=1).  In the
+// real build a stamp compiles to nothing.
+struct Stamper {
+#ifdef KMC_STAMPS
+  uint64_t t;
+  int base;
+  __device__ static uint64_t now() {
+    uint64_t v;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");
+    return v;
+  }
+  __device__ explicit Stamper(int b) : t(now()), base(b) {}
+  __device__ void operator()(const Dev& d, int i) {
+    if (threadIdx.x == 0) {
+      const uint64_t v = now();
+      atomicAdd((unsigned long long*)&d.ctl->stamps[base + i], (unsigned long long)(v - t));
+      t = v;
+    }
+  }
+#else
+  __device__ explicit Stamper(int) {}
+  __device__ void operator()(const Dev&, int) {}
+#endif
+};
+
 // ---------------------------------------------------------------- LDS tiles
 // Records are sorted by (cell row, kind, cell column) — cell_index() — so the
 // records of one kind in a run of columns of one row are contiguous.
@@ -1298,13 +1327,12 @@ __device__ __forceinline__ void wg_flush(WgList& L, const SList& out, uint32_t* 
 // hold a partner) — into an LDS pair list (one wave-level prefix sum + one
 // LDS atomic per wave), and the pairs are checked with every lane busy.  A
 // record whose pairs do not fit the list is scanned in place.
-#define TILE_MAX 16
+#define TILE_MAX 14
 #define HALO_MAX (TILE_MAX + 2)
 #define NSEG_MAX (2 * HALO_MAX)
-#define TCAP 1024
+#define TCAP 768
 #define PCAP 2048
 #define PAIR_NONE 0xffffffffu
-#define RID_FIN (1 << 24)  // staged record is its protein's final position (reaction scan)
 struct TileLds {
   float4 pos[TCAP];
   int2 id[TCAP];
@@ -1325,7 +1353,8 @@ __device__ __forceinline__ int tile_global(const TileLds& T, int l) { return l +
 // Returns false (uniformly) when the tile holds more than P.tcap records; the
 // caller then takes the global-memory path.  site (reaction scan only): the
 // [3][3] site of each record; its final flag goes into id.x as RID_FIN.
-__device__ bool tile_load(const KParams& P, const Dev& d, int tx, int ty, TileLds& T, float2* site, uint32_t step) {
+__device__ bool tile_load(const KParams& P, const Dev& d, int tx, int ty, TileLds& T, float2* site, uint32_t step,
+                          Stamper& S) {
   const int tile = P.tile, halo = tile + 2, nseg = 2 * halo;
   const int cx0 = tx * tile - 1, cy0 = ty * tile - 1;
   const int xlo = max(cx0, 0), xhi = min(cx0 + halo - 1, P.ncx - 1);
@@ -1341,6 +1370,7 @@ __device__ bool tile_load(const KParams& P, const Dev& d, int tx, int ty, TileLd
     T.cstart[seg][hx] = v;
   }
   __syncthreads();
+  S(d, 0);
   if (threadIdx.x < 64) {  // segment lengths -> LDS segment bases (wave-0 inclusive scan)
     int seg = threadIdx.x;
     int len = seg < nseg ? T.cstart[seg][halo] - T.cstart[seg][0] : 0;
@@ -1354,11 +1384,13 @@ __device__ bool tile_load(const KParams& P, const Dev& d, int tx, int ty, TileLd
     if (seg == nseg - 1) T.n = inc;
   }
   __syncthreads();
+  S(d, 1);
   for (int idx = threadIdx.x; idx < nseg * (halo + 1); idx += blockDim.x) {
     int seg = idx / (halo + 1), hx = idx - seg * (halo + 1);
     T.cstart[seg][hx] -= T.goff[seg];
   }
   __syncthreads();
+  S(d, 2);
   const int n = T.n;
   if (n > P.tcap) return false;
   for (int idx = threadIdx.x; idx < nseg * halo; idx += blockDim.x) {  // tags: one thread per cell
@@ -1366,6 +1398,7 @@ __device__ bool tile_load(const KParams& P, const Dev& d, int tx, int ty, TileLd
     for (int l = T.cstart[seg][hx]; l < T.cstart[seg][hx + 1]; ++l) T.tag[l] = (uint16_t)(seg | hx << 8);
   }
   __syncthreads();
+  S(d, 3);
   // four records per thread in flight: loads from clamped indices first, then
   // the LDS stores (keeps the staging arrays in registers)
   for (int base = 0; base < n; base += 4 * blockDim.x) {
@@ -1379,17 +1412,14 @@ __device__ bool tile_load(const KParams& P, const Dev& d, int tx, int ty, TileLd
     for (int k = 0; k < 4; ++k) {
       int l = base + k * (int)blockDim.x + (int)threadIdx.x;
       if (l < n) {
-        int2 id = rc[k].id;
-        if (site) {
-          site[l] = rc[k].site;
-          if ((id.x < 0) != (d.rejtag[id.x & RID_PID] == step)) id.x |= RID_FIN;
-        }
+        if (site) site[l] = rc[k].site;
         T.pos[l] = rc[k].pos;
-        T.id[l] = id;
+        T.id[l] = rc[k].id;
       }
     }
   }
   __syncthreads();
+  S(d, 4);
   return true;
 }
 
@@ -1564,7 +1594,8 @@ __global__ void __launch_bounds__(256) k_col_scan(KParams P, Dev d) {
   const int ntx = (P.ncx + P.tile - 1) / P.tile;
   const int tx = blockIdx.x % ntx, ty = blockIdx.x / ntx;
   wg_list_init(L);
-  if (tile_load(P, d, tx, ty, T, nullptr, 0)) {
+  Stamper S(0);
+  if (tile_load(P, d, tx, ty, T, nullptr, 0, S)) {
     if (P.dbg_stage == 1) return;
     // proposal records and their cut stencils
     tile_pairs(
@@ -1593,6 +1624,7 @@ __global__ void __launch_bounds__(256) k_col_scan(KParams P, Dev d) {
               else col_emit(d, L, tile_global(T, l), tile_global(T, r));
             }
         });
+    S(d, 5);
     if (P.dbg_stage == 2) return;
     const uint32_t np = min(T.npair, (uint32_t)PCAP);
     PairBuf B;
@@ -1609,8 +1641,10 @@ __global__ void __launch_bounds__(256) k_col_scan(KParams P, Dev d) {
     }
     pair_flush(B, L, d.cand, &d.ctl->err,
                [&](int2 v) { return make_int2(tile_global(T, v.x), tile_global(T, v.y)); });
+    S(d, 6);
     if (P.dbg_stage == 3) return;
     wg_flush(L, d.cand, &d.ctl->err);
+    S(d, 7);
     return;
   }
   // dense tile: one thread per interior cell, records from global memory
@@ -1749,10 +1783,20 @@ __global__ void __launch_bounds__(1024) k_col_tail(KParams P, Dev d, int round0)
 }
 
 // ================================================================ 5. commit
-// The members of every rejected unit get this step's reject tag (their final
-// position is the old one); untouched units were accepted.
+// The members of every rejected unit: their final position is the old one.
+// Lanes 0 / 1 move the final flag (RID_FIN) of the member's two records from
+// the proposal record (set by k_rec_scatter) to the old one — the reaction
+// scan reads finality from the records — then R is copied to R_new.
 __device__ __forceinline__ void rej_member(const KParams& P, const Dev& d, int m, uint32_t step, int lane) {
-  if (lane == 0) d.rejtag[m] = step;
+  const int NA = P.NA;
+  if (lane < 2) {
+    const Beads& B = lane ? d.nxt : d.cur;
+    const double x = B.P(m, 1, 1, 0), y = B.P(m, 1, 1, 1);
+    const int2 rk = d.rank[m];
+    const int pos = d.cell_start[rec_cell(P, x, y, m >= NA)] + (lane ? rk.y : rk.x);
+    const int st = m < NA ? (A_ST2(d, m) ? RID_ST2 : 0) | (A_ST3(d, m) ? RID_ST3 : 0) : 0;
+    d.rec[pos].id.x = m | st | (lane ? (int)0x80000000 : RID_FIN);
+  }
   const bool a = m < P.NA;
   const int n = a ? P.NA : P.NB, i = a ? m : m - P.NA, rows = a ? 48 : 24;
   const double* src = a ? d.cur.a : d.cur.b;
@@ -1784,7 +1828,7 @@ __global__ void k_rej_commit(KParams P, Dev d) {
 
 // ================================================================ 6. reactions
 __device__ __forceinline__ bool record_final(const Dev& d, int2 id, uint32_t step) {
-  return (id.x < 0) != (d.rejtag[id.x & RID_PID] == step);
+  return (id.x & RID_FIN) != 0;
 }
 
 // Reaction candidates, pass 1 (tiled): the final-position record of every
@@ -1836,7 +1880,8 @@ __global__ void __launch_bounds__(256) k_rxn_scan_tile(KParams P, Dev d) {
   const int NA = P.NA, NB = P.NB;
   const uint32_t step = d.ctl->step;
   wg_list_init(L);
-  if (tile_load(P, d, tx, ty, T, site, step)) {
+  Stamper S(8);
+  if (tile_load(P, d, tx, ty, T, site, step, S)) {
     if (P.dbg_stage == 1) return;
     // final receptor records that can still react, and their cut stencils
     tile_pairs(
@@ -1862,6 +1907,7 @@ __global__ void __launch_bounds__(256) k_rxn_scan_tile(KParams P, Dev d) {
                 rxn_emit(d, L, me.x & RID_PID, id.x & RID_PID);
             }
         });
+    S(d, 5);
     if (P.dbg_stage == 2) return;
     const uint32_t np = min(T.npair, (uint32_t)PCAP);
     PairBuf B;
@@ -1877,8 +1923,10 @@ __global__ void __launch_bounds__(256) k_rxn_scan_tile(KParams P, Dev d) {
       else rxn_emit(d, L, v.x, v.y);
     }
     pair_flush(B, L, d.pairs, &d.ctl->err, [](int2 v) { return v; });
+    S(d, 6);
     if (P.dbg_stage == 3) return;
     wg_flush(L, d.pairs, &d.ctl->err);
+    S(d, 7);
     return;
   }
   for (int c = threadIdx.x; c < P.tile * P.tile; c += blockDim.x) {
