@@ -13,7 +13,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libkmc.so")
+# KMC_LIB_PATH: diagnostic builds only (e.g. the -DKMC_STAMPS timing build)
+LIB_PATH = os.environ.get("KMC_LIB_PATH") or os.path.join(HERE, "lib", "libkmc.so")
 
 KMC_OK = 0
 ERRORS = {
