@@ -69,20 +69,43 @@ enum : uint8_t { U_NONE = 0, U_FREE_A = 1, U_DIMER = 2, U_FREE_B = 3, U_COMPLEX 
 enum : uint32_t { S_ACC = 1, S_PEND = 2, S_REJ = 3 };  // unit fate this step (atomicMax order)
 
 // ---------------------------------------------------------------- layout
-// Receptor bead (j,k) (1-based) coordinate c lives at
-//   a[((((j-1)*4 + (k-1))*3 + c) * NA + i];   ligand at b[(((j-1)*2+(k-1))*3+c)*NB + i]
-// i.e. structure-of-arrays per bead coordinate: a wave's 64 lanes (64
-// consecutive proteins) load 512 contiguous bytes per bead coordinate.
+// Paired structure-of-arrays: every element is a double2 holding two
+// coordinates of ONE protein, so a lane moves 16 bytes per access (one
+// dwordx4) and a wave 1 KiB contiguous.  Element (row r, slot i) is double2
+// number r·n + i (n = NA or NB).  Receptor rows (bead (j,k), 1-based):
+//   (j-1)·4 + (k-1)              (x, y) of bead (j,k)                rows 0..15
+//   16 + (j-1)/2·4 + (k-1), j odd (z of (j,k), z of (j+1,k))         rows 16..23
+// Ligand rows: (j-1)·2 + (k-1) (x, y), rows 0..7; 8 + (j-1)/2·2 + (k-1) the z
+// pairs, rows 8..11.  The host side (kmc_state_view) keeps the reference-order
+// SoA `[(bead·3 + c)][n]`; k_gather_beads converts at the boundary.
+#define ROWS_A 24
+#define ROWS_B 12
+__host__ __device__ __forceinline__ size_t bead_off_a(int i, int j, int k, int c, int NA) {
+  const int row = c < 2 ? (j - 1) * 4 + (k - 1) : 16 + ((j - 1) >> 1) * 4 + (k - 1);
+  const int half = c < 2 ? c : ((j - 1) & 1);
+  return ((size_t)row * NA + i) * 2 + half;
+}
+__host__ __device__ __forceinline__ size_t bead_off_b(int i, int j, int k, int c, int NB) {
+  const int row = c < 2 ? (j - 1) * 2 + (k - 1) : 8 + ((j - 1) >> 1) * 2 + (k - 1);
+  const int half = c < 2 ? c : ((j - 1) & 1);
+  return ((size_t)row * NB + i) * 2 + half;
+}
 struct Beads {
   double* a;
   double* b;
   int NA, NB;
-  __device__ __forceinline__ double& A(int i, int j, int k, int c) const {
-    return a[(size_t)((((j - 1) * 4 + (k - 1)) * 3) + c) * NA + i];
+  __device__ __forceinline__ double& A(int i, int j, int k, int c) const { return a[bead_off_a(i, j, k, c, NA)]; }
+  __device__ __forceinline__ double& B(int i, int j, int k, int c) const { return b[bead_off_b(i, j, k, c, NB)]; }
+  // whole double2 rows (one 16-byte access)
+  __device__ __forceinline__ double2& A2(int i, int row) const {
+    return reinterpret_cast<double2*>(a)[(size_t)row * NA + i];
   }
-  __device__ __forceinline__ double& B(int i, int j, int k, int c) const {
-    return b[(size_t)((((j - 1) * 2 + (k - 1)) * 3) + c) * NB + i];
+  __device__ __forceinline__ double2& B2(int i, int row) const {
+    return reinterpret_cast<double2*>(b)[(size_t)row * NB + i];
   }
+  // (x, y) of a bead in one access
+  __device__ __forceinline__ double2 Axy(int i, int j, int k) const { return A2(i, (j - 1) * 4 + (k - 1)); }
+  __device__ __forceinline__ double2 Bxy(int i, int j, int k) const { return B2(i, (j - 1) * 2 + (k - 1)); }
   // protein p is 0-based over [0, NA+NB)
   __device__ __forceinline__ double& P(int p, int j, int k, int c) const {
     return p < NA ? A(p, j, k, c) : B(p - NA, j, k, c);

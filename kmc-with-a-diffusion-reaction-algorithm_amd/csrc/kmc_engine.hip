@@ -342,19 +342,21 @@ int64_t kmc_current_step(const kmc_sim* s) { return s ? s->step_done : -1; }
 
 // Gather R, the state rows and bond fields through perm (new index -> old
 // slot) into R_new / scratch, renumbering bond fields through map, and swap.
+// swap_in (re-sort): beads stay in the device layout; otherwise (get_state)
+// they come out in the host layout of kmc_state_view.
 static void reorder(kmc_sim* s, const int32_t* perm, const int32_t* map, bool swap_in) {
   const KParams& K = s->K;
   Dev& d = s->d;
   hipStream_t st = s->stream;
-  const int NA = K.NA, NB = K.NB, T = 256;
+  const int NA = K.NA, NB = K.NB, T = 256, mode = swap_in ? 0 : 1;
   auto g = [&](size_t n) { return (unsigned)((n + T - 1) / T); };
   if (NA > 0) {
-    k_gather_f64<<<g((size_t)48 * NA), T, 0, st>>>(d.cur.a, d.nxt.a, perm, 0, NA, 48);
+    k_gather_beads<<<g((size_t)(swap_in ? ROWS_A : 48) * NA), T, 0, st>>>(d.cur.a, d.nxt.a, perm, 0, NA, 0, mode);
     // a rows: st2 st3 nei2 nei4 nei3 (nei2, nei3 are protein links)
     k_gather_i32<<<g((size_t)5 * NA), T, 0, st>>>(d.a_int, s->a_tmp, perm, 0, NA, 5, (1u << 2) | (1u << 4), map);
   }
   if (NB > 0) {
-    k_gather_f64<<<g((size_t)24 * NB), T, 0, st>>>(d.cur.b, d.nxt.b, perm, NA, NB, 24);
+    k_gather_beads<<<g((size_t)(swap_in ? ROWS_B : 24) * NB), T, 0, st>>>(d.cur.b, d.nxt.b, perm, NA, NB, 1, mode);
     k_gather_i32<<<g((size_t)8 * NB), T, 0, st>>>(d.b_int, s->b_tmp, perm, NA, NB, 8, 0xf0u, map);
   }
   if (!swap_in) return;
@@ -397,8 +399,10 @@ int kmc_set_state(kmc_sim* s, const kmc_state_view* v) {
   if (rc != KMC_OK) return rc;
   const int NA = s->p.n_a, NB = s->p.n_b;
   Dev& d = s->d;
-  HIPCHK(s, hipMemcpy(d.cur.a, v->ra, sizeof(double) * 48 * (size_t)NA, hipMemcpyHostToDevice));
-  HIPCHK(s, hipMemcpy(d.cur.b, v->rb, sizeof(double) * 24 * (size_t)NB, hipMemcpyHostToDevice));
+  // beads arrive in the host layout: into the scratch buffers, converted to
+  // the device layout below
+  HIPCHK(s, hipMemcpy(d.nxt.a, v->ra, sizeof(double) * 48 * (size_t)NA, hipMemcpyHostToDevice));
+  HIPCHK(s, hipMemcpy(d.nxt.b, v->rb, sizeof(double) * 24 * (size_t)NB, hipMemcpyHostToDevice));
   HIPCHK(s, hipMemcpy(d.a_int, v->a_int, sizeof(int32_t) * 5 * (size_t)NA, hipMemcpyHostToDevice));
   HIPCHK(s, hipMemcpy(d.b_int, v->b_int, sizeof(int32_t) * 8 * (size_t)NB, hipMemcpyHostToDevice));
   int rl, mono, cis;
@@ -418,6 +422,12 @@ int kmc_set_state(kmc_sim* s, const kmc_state_view* v) {
   HIPCHK(s, hipMemset(d.moved, 0, sizeof(uint32_t) * (size_t)(NA + NB)));
   // reference order = identity slots, then the spatial sort
   k_iota<<<(NA + NB + 255) / 256, 256, 0, s->stream>>>(d.id_of, d.slot_of, NA + NB);
+  if (NA > 0)
+    k_gather_beads<<<(unsigned)((48 * (size_t)NA + 255) / 256), 256, 0, s->stream>>>(d.nxt.a, d.cur.a, d.id_of, 0,
+                                                                                     NA, 0, 2);
+  if (NB > 0)
+    k_gather_beads<<<(unsigned)((24 * (size_t)NB + 255) / 256), 256, 0, s->stream>>>(d.nxt.b, d.cur.b, d.id_of, NA,
+                                                                                     NB, 1, 2);
   rc = resort(s);
   if (rc != KMC_OK) return rc;
   HIPCHK(s, hipStreamSynchronize(s->stream));

@@ -288,14 +288,16 @@ __device__ __forceinline__ int bfs_overflow_one(const KParams& P, const Dev& d, 
 __device__ __forceinline__ void ref_point(const Dev& d, const Beads& B, int p, int NA, double& x, double& y,
                                           double& zlo, double& zhi) {
   if (p < NA) {
-    x = B.A(p, 1, 1, 0);
-    y = B.A(p, 1, 1, 1);
-    double z1 = B.A(p, 1, 1, 2), z2 = B.A(p, 2, 1, 2), z3 = B.A(p, 3, 1, 2), z4 = B.A(p, 4, 1, 2);
+    const double2 xy = B.Axy(p, 1, 1), z12 = B.A2(p, 16), z34 = B.A2(p, 20);  // z of domains 1,2 / 3,4
+    x = xy.x;
+    y = xy.y;
+    double z1 = z12.x, z2 = z12.y, z3 = z34.x, z4 = z34.y;
     zlo = fmin(fmin(z1, z2), fmin(z3, z4));  // the axis span of the four domains
     zhi = fmax(fmax(z1, z2), fmax(z3, z4));
   } else {
-    x = B.B(p - NA, 1, 1, 0);
-    y = B.B(p - NA, 1, 1, 1);
+    const double2 xy = B.Bxy(p - NA, 1, 1);
+    x = xy.x;
+    y = xy.y;
     zlo = B.B(p - NA, 1, 1, 2);
     zhi = zlo;
   }
@@ -353,17 +355,27 @@ __device__ __forceinline__ void count_new(const KParams& P, const Dev& d, int p,
   if (!ext) atomicOr(&d.ctl->err, ERR_GEOMETRY);
 }
 
-// free receptor, main.cpp:584-635.  All 48 coordinates are loaded before the
-// first store (R and R_new are distinct buffers), so a lane has every load in
-// flight at once.
+// free receptor, main.cpp:584-635.  All 48 coordinates are loaded (24 16-byte
+// rows) before the first store (R and R_new are distinct buffers), so a lane
+// has every load in flight at once.
 __device__ void propose_free_a(const KParams& P, const Dev& d, int i, uint32_t step) {
   double r[4][4][3];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
+    for (int k = 0; k < 4; ++k) {
+      const double2 v = d.cur.A2(i, j * 4 + k);
+      r[j][k][0] = v.x;
+      r[j][k][1] = v.y;
+    }
 #pragma unroll
-      for (int c = 0; c < 3; ++c) r[j][k][c] = d.cur.A(i, j + 1, k + 1, c);
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const double2 v = d.cur.A2(i, 16 + h * 4 + k);
+      r[2 * h][k][2] = v.x;
+      r[2 * h + 1][k][2] = v.y;
+    }
   const int rk_old = atomicAdd(&d.cell_cnt[rec_cell(P, r[0][0][0], r[0][0][1], 0)], 1);
   double u0, u1, u2, u3;
   const uint32_t ri = (uint32_t)d.id_of[i];
@@ -376,7 +388,7 @@ __device__ void propose_free_a(const KParams& P, const Dev& d, int i, uint32_t s
   double PBx = P.box_x * kmcm::round_(o11x / P.box_x);
   double PBy = P.box_y * kmcm::round_(o11y / P.box_y);
   Rot t = euler(0, 0, (2 * u2 - 1) * P.rot_a);
-  double ncx[4], ncy[4];
+  double ncx[4], ncy[4], nz[4][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     double cx = (r[j][0][0] + dx) - PBx;
@@ -384,19 +396,21 @@ __device__ void propose_free_a(const KParams& P, const Dev& d, int i, uint32_t s
     double cz = r[j][0][2];
     ncx[j] = cx;
     ncy[j] = cy;
-    d.nxt.A(i, j + 1, 1, 0) = cx;
-    d.nxt.A(i, j + 1, 1, 1) = cy;
-    d.nxt.A(i, j + 1, 1, 2) = cz;
+    nz[j][0] = cz;
+    d.nxt.A2(i, j * 4) = make_double2(cx, cy);
 #pragma unroll
     for (int k = 1; k < 4; ++k) {
       double ox = (r[j][k][0] + dx) - PBx;
       double oy = (r[j][k][1] + dy) - PBy;
       double oz = r[j][k][2];
-      d.nxt.A(i, j + 1, k + 1, 0) = rx(t, ox, oy, oz, cx, cy, cz);
-      d.nxt.A(i, j + 1, k + 1, 1) = ry(t, ox, oy, oz, cx, cy, cz);
-      d.nxt.A(i, j + 1, k + 1, 2) = rz(t, ox, oy, oz, cx, cy, cz);
+      d.nxt.A2(i, j * 4 + k) = make_double2(rx(t, ox, oy, oz, cx, cy, cz), ry(t, ox, oy, oz, cx, cy, cz));
+      nz[j][k] = rz(t, ox, oy, oz, cx, cy, cz);
     }
   }
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) d.nxt.A2(i, 16 + h * 4 + k) = make_double2(nz[2 * h][k], nz[2 * h + 1][k]);
   bool ext = true;
 #pragma unroll
   for (int j = 1; j < 4; ++j) {
@@ -518,15 +532,26 @@ __device__ __forceinline__ void propose_dimer(const KParams& P, const Dev& d, in
   if (!AreSame(dist1, dist3) || !AreSame(dist2, dist4)) snap_cis(P, d.nxt, q, i, P.cis_cut);
 }
 
-// single ligand, main.cpp:905-969 (all 24 coordinates loaded first)
+// single ligand, main.cpp:905-969 (all 24 coordinates, 12 16-byte rows,
+// loaded first)
 __device__ void propose_free_b(const KParams& P, const Dev& d, int lb, int p, uint32_t step) {
   double r[4][2][3];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
-    for (int k = 0; k < 2; ++k)
+    for (int k = 0; k < 2; ++k) {
+      const double2 v = d.cur.B2(lb, j * 2 + k);
+      r[j][k][0] = v.x;
+      r[j][k][1] = v.y;
+    }
 #pragma unroll
-      for (int c = 0; c < 3; ++c) r[j][k][c] = d.cur.B(lb, j + 1, k + 1, c);
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const double2 v = d.cur.B2(lb, 8 + h * 2 + k);
+      r[2 * h][k][2] = v.x;
+      r[2 * h + 1][k][2] = v.y;
+    }
   const int rk_old = atomicAdd(&d.cell_cnt[rec_cell(P, r[0][0][0], r[0][0][1], 1)], 1);
   double u[6];
   const uint32_t rp = (uint32_t)d.id_of[p];
@@ -561,6 +586,7 @@ __device__ void propose_free_b(const KParams& P, const Dev& d, int lb, int p, ui
   // updates the centre in place) rotates about R_new[1][1], main.cpp:958-968
   double cx = ox[0][0], cy = oy[0][0], cz = oz[0][0];
   double scx[4], scy[4];  // new subunit centres [j][1] (extent bound)
+  double nzs[4][2];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -575,10 +601,13 @@ __device__ void propose_free_b(const KParams& P, const Dev& d, int lb, int p, ui
         scx[j] = nx;
         scy[j] = ny;
       }
-      d.nxt.B(lb, j + 1, k + 1, 0) = nx;
-      d.nxt.B(lb, j + 1, k + 1, 1) = ny;
-      d.nxt.B(lb, j + 1, k + 1, 2) = nz;
+      d.nxt.B2(lb, j * 2 + k) = make_double2(nx, ny);
+      nzs[j][k] = nz;
     }
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) d.nxt.B2(lb, 8 + h * 2 + k) = make_double2(nzs[2 * h][k], nzs[2 * h + 1][k]);
   bool ext = true;
 #pragma unroll
   for (int j = 1; j < 4; ++j) {
@@ -1109,25 +1138,32 @@ struct Own {
 };
 __device__ __forceinline__ void load_own(const KParams& P, const Beads& B, int m, Own& o) {
   o.isA = m < P.NA;
+  // [k][1] beads: (x, y) rows, z of domains / subunits 1,2 and 3,4 in two rows
+  double2 z12, z34;
   if (o.isA) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      o.x[k] = B.A(m, k + 1, 1, 0);
-      o.y[k] = B.A(m, k + 1, 1, 1);
-      o.z[k] = B.A(m, k + 1, 1, 2);
+      const double2 xy = B.Axy(m, k + 1, 1);
+      o.x[k] = xy.x;
+      o.y[k] = xy.y;
     }
+    z12 = B.A2(m, 16);
+    z34 = B.A2(m, 20);
   } else {
     int b = m - P.NA;
-    o.x[0] = B.B(b, 1, 1, 0);
-    o.y[0] = B.B(b, 1, 1, 1);
-    o.z[0] = B.B(b, 1, 1, 2);
 #pragma unroll
-    for (int k = 1; k < 4; ++k) {
-      o.x[k] = B.B(b, k + 1, 1, 0);
-      o.y[k] = B.B(b, k + 1, 1, 1);
-      o.z[k] = B.B(b, k + 1, 1, 2);
+    for (int k = 0; k < 4; ++k) {
+      const double2 xy = B.Bxy(b, k + 1, 1);
+      o.x[k] = xy.x;
+      o.y[k] = xy.y;
     }
+    z12 = B.B2(b, 8);
+    z34 = B.B2(b, 10);
   }
+  o.z[0] = z12.x;
+  o.z[1] = z12.y;
+  o.z[2] = z34.x;
+  o.z[3] = z34.y;
 }
 
 __device__ bool exact_collide(const KParams& P, const Own& o, const Beads& B, int q) {
@@ -1798,9 +1834,9 @@ __device__ __forceinline__ void rej_member(const KParams& P, const Dev& d, int m
     d.rec[pos].id.x = m | st | (lane ? (int)0x80000000 : RID_FIN);
   }
   const bool a = m < P.NA;
-  const int n = a ? P.NA : P.NB, i = a ? m : m - P.NA, rows = a ? 48 : 24;
-  const double* src = a ? d.cur.a : d.cur.b;
-  double* dst = a ? d.nxt.a : d.nxt.b;
+  const int n = a ? P.NA : P.NB, i = a ? m : m - P.NA, rows = a ? ROWS_A : ROWS_B;
+  const double2* src = reinterpret_cast<const double2*>(a ? d.cur.a : d.cur.b);
+  double2* dst = reinterpret_cast<double2*>(a ? d.nxt.a : d.nxt.b);
   if (lane < rows) dst[(size_t)lane * n + i] = src[(size_t)lane * n + i];  // R_new = R
 }
 
@@ -2381,12 +2417,27 @@ __global__ void k_slot_inverse(KParams P, const int32_t* sorted, int32_t* perm, 
   newslot[old] = s;
 }
 
-// rows of a [rows][n] array gathered through perm (offset: kind's first slot)
-__global__ void k_gather_f64(const double* in, double* out, const int32_t* perm, int off, int n, int rows) {
-  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (size_t)n * rows) return;
-  int r = (int)(t / n), s = (int)(t % n);
-  out[(size_t)r * n + s] = in[(size_t)r * n + (perm[off + s] - off)];
+// Bead arrays of one kind gathered through perm (offset: the kind's first
+// slot).  mode 0: device layout (kmc_device.h §layout) in and out, one double2
+// row element per thread; 1: device layout in, host layout out (the
+// reference-order SoA [bead·3 + c][n] of kmc_state_view); 2: host in, device out.
+__global__ void k_gather_beads(const double* in, double* out, const int32_t* perm, int off, int n, int ligand,
+                               int mode) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (mode == 0) {
+    if (t >= (size_t)n * (ligand ? ROWS_B : ROWS_A)) return;
+    const int r = (int)(t / n), s = (int)(t % n);
+    reinterpret_cast<double2*>(out)[(size_t)r * n + s] =
+        reinterpret_cast<const double2*>(in)[(size_t)r * n + (perm[off + s] - off)];
+    return;
+  }
+  if (t >= (size_t)n * (ligand ? 24 : 48)) return;
+  const int q = (int)(t / n), s = (int)(t % n), src = perm[off + s] - off;
+  const int bead = q / 3, c = q % 3, nk = ligand ? 2 : 4, j = bead / nk + 1, k = bead % nk + 1;
+  if (mode == 1)
+    out[(size_t)q * n + s] = in[ligand ? bead_off_b(src, j, k, c, n) : bead_off_a(src, j, k, c, n)];
+  else
+    out[ligand ? bead_off_b(s, j, k, c, n) : bead_off_a(s, j, k, c, n)] = in[(size_t)q * n + src];
 }
 
 // bond/state rows; rows flagged in link_mask hold protein index + 1 (0 = none)
