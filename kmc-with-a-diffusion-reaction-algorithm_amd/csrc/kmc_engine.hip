@@ -229,6 +229,8 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   rc |= dalloc(s, &d.overflow, NB);
   rc |= dalloc(s, &d.cx_list, NB);
   rc |= dalloc(s, &d.cell_cnt, s->ncell + 1);
+  rc |= dalloc(s, &d.cell_cnt_alt, s->ncell + 1);
+  d.ncnt = s->ncell + 1;
   rc |= dalloc(s, &d.cell_start, s->ncell + 1);
   rc |= dalloc(s, &d.block_sums, s->nscan_blocks);
   rc |= dalloc(s, &d.rec, (size_t)2 * N);
@@ -612,6 +614,7 @@ static int launch_step(kmc_sim* s, bool re_sort) {
   if (s->tnow) s->tslot = (s->tslot + 1) % TRING;
   // R_new becomes R (main.cpp:2164-2191): swap the bead buffers
   std::swap(d.cur, d.nxt);
+  std::swap(d.cell_cnt, d.cell_cnt_alt);
   return KMC_OK;
 }
 
