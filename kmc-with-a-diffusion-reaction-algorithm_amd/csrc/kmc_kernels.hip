@@ -1126,22 +1126,40 @@ __global__ void k_rec_scatter(KParams P, Dev d) {
   int st = 0;
   if (p < NA) st = (A_ST2(d, p) ? RID_ST2 : 0) | (A_ST3(d, p) ? RID_ST3 : 0);
   const int2 rk = d.rank[p];
+  const int own = d.owner[p];
+  // both records' loads are issued before either store (two independent
+  // load -> cell -> cell_start chains in flight per lane)
+  double x[2], y[2], zl[2], zh[2];
+  float2 site[2];
+  int pos[2], end[2];
+#pragma unroll
   for (int w = 0; w < 2; ++w) {
-    double x, y, zl, zh;
-    ref_point(d, w ? d.nxt : d.cur, p, P.NA, x, y, zl, zh);
-    int c = rec_cell(P, x, y, p >= NA);
-    const int r = w ? rk.y : rk.x;
-    int pos = d.cell_start[c] + r;
-    if (r < 0 || pos >= d.cell_start[c + 1]) {  // a protein no unit counted: inconsistent bond graph
+    const Beads& B = w ? d.nxt : d.cur;
+    ref_point(d, B, p, NA, x[w], y[w], zl[w], zh[w]);
+    if (p < NA) {
+      const double2 s33 = B.Axy(p, 3, 3);
+      site[w] = make_float2((float)s33.x, (float)s33.y);
+    } else {
+      site[w] = make_float2(0.f, 0.f);
+    }
+  }
+#pragma unroll
+  for (int w = 0; w < 2; ++w) {
+    const int c = rec_cell(P, x[w], y[w], p >= NA);
+    pos[w] = d.cell_start[c] + (w ? rk.y : rk.x);
+    end[w] = d.cell_start[c + 1];
+  }
+#pragma unroll
+  for (int w = 0; w < 2; ++w) {
+    if ((w ? rk.y : rk.x) < 0 || pos[w] >= end[w]) {  // a protein no unit counted: inconsistent bond graph
       atomicOr(&d.ctl->err, ERR_RESOLVE);
       continue;
     }
-    const Beads& B = w ? d.nxt : d.cur;
     Rec rc;
-    rc.pos = make_float4((float)x, (float)y, (float)zl, (float)zh);
-    rc.id = make_int2(p | st | (w << 31) | (w ? RID_FIN : 0), d.owner[p]);
-    rc.site = p < NA ? make_float2((float)B.A(p, 3, 3, 0), (float)B.A(p, 3, 3, 1)) : make_float2(0.f, 0.f);
-    d.rec[pos] = rc;  // one 32-byte store
+    rc.pos = make_float4((float)x[w], (float)y[w], (float)zl[w], (float)zh[w]);
+    rc.id = make_int2(p | st | (w << 31) | (w ? RID_FIN : 0), own);
+    rc.site = site[w];
+    d.rec[pos[w]] = rc;  // one 32-byte store
   }
 }
 
