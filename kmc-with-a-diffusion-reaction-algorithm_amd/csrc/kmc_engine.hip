@@ -582,9 +582,8 @@ static int launch_step(kmc_sim* s, bool re_sort) {
   if (K.NB > 0) {
     TIMED(KI_BFS, (k_bfs<<<gB, T, 0, st>>>(K, d)));
   }
-  // complexes (one wave each), then the free units
-  if (K.NB > 0) TIMED(KI_COMPLEX, (k_complex<<<K.cx_blocks, T, 0, st>>>(K, d)));
-  TIMED(KI_PROPOSE, (k_propose<<<gN, T, 0, st>>>(K, d)));
+  // complexes (one wave each) and the free units in one launch
+  TIMED(KI_PROPOSE, (k_propose<<<K.cx_blocks + gN, T, 0, st>>>(K, d)));
   TIMED(KI_SCAN, {
     // single-pass decoupled look-back scan; cell_cnt[ncell] stays 0, so
     // cell_start[ncell] is the record total

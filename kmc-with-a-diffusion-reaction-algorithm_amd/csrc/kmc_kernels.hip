@@ -637,8 +637,7 @@ __device__ void propose_free_b(const KParams& P, const Dev& d, int lb, int p, ui
 
 // One thread per slot: free receptors, cis dimers and free ligands (the
 // complexes were moved by k_complex just before).
-__global__ void __launch_bounds__(256) k_propose(KParams P, Dev d) {
-  int p = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void propose_one(const KParams& P, const Dev& d, int p) {
   if (p >= P.N) return;
   const uint32_t step = d.ctl->step;
   const int NA = P.NA;
@@ -1037,11 +1036,11 @@ __device__ __forceinline__ void complex_wave(const KParams& P, const Dev& d, int
   for (int t2 = lane; t2 < csize; t2 += 64) count_records(P, d, res[t2]);
 }
 
-// P.cx_blocks workgroups; each wave takes complexes from the BFS's root list.
+// nblk workgroups; each wave takes complexes from the BFS's root list.
 // Wave 0 first runs the BFS of the components that overflowed k_bfs's
 // register queue (rare: > BFS_QCAP members) and moves those it roots.
-__global__ void __launch_bounds__(256) k_complex(KParams P, Dev d) {
-  const int w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), nw = gridDim.x * (blockDim.x >> 6);
+__device__ __forceinline__ void complex_waves(const KParams& P, const Dev& d, int blk, int nblk) {
+  const int w = blk * (blockDim.x >> 6) + (threadIdx.x >> 6), nw = nblk * (blockDim.x >> 6);
   const uint32_t n = d.ctl->n_cx;
   if (w == 0) {
     const uint32_t no = d.ctl->n_overflow;
@@ -1053,6 +1052,19 @@ __global__ void __launch_bounds__(256) k_complex(KParams P, Dev d) {
     }
   }
   for (uint32_t c = w; c < n; c += nw) complex_wave(P, d, d.cx_list[c], __lane_id());
+}
+// Complexes (the first cx_blocks workgroups, dispatched first; 0 without
+// ligands) and the free units (the rest, one thread per slot) in one launch:
+// the complexes' latency-bound waves overlap the free units' HBM stream
+// (measured 0.514 -> 0.494 ms/step at C3 against two launches; a side stream
+// was slower).  The two sets of proteins are disjoint and the record counts
+// are commutative atomics.
+__global__ void __launch_bounds__(256) k_propose(KParams P, Dev d) {
+  if ((int)blockIdx.x < P.cx_blocks) {
+    complex_waves(P, d, blockIdx.x, P.cx_blocks);
+    return;
+  }
+  propose_one(P, d, ((int)blockIdx.x - P.cx_blocks) * blockDim.x + threadIdx.x);
 }
 
 // exclusive scan of cell_cnt[0..n) into cell_start[0..n]; 3 kernels
