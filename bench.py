@@ -1,20 +1,32 @@
 """Benchmark: KMC particle-updates/s of the HIP engine (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload C3]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload C3] [--evolve E]
 
-One process per GPU (launched by torch.distributed.run for N > 1), each
-running an independent replica trajectory (key = (seed, rank)) of the
-workload — SURVEY.md §8(e) "replicas only" — with one RCCL all-reduce of the
-ensemble observables per timed batch.  Prints ONE JSON line (rank 0):
+Ranks.  One process per GPU, each an independent replica trajectory (key =
+(seed, rank)) — SURVEY.md §8(e) "replicas only" — with one RCCL all-reduce of
+the ensemble observables per timed batch.  Under torch.distributed.run
+(WORLD_SIZE set) this process is one rank and --gpus must equal WORLD_SIZE.
+Without it and --gpus N > 1, this process is a GPU-free launcher: it checks
+that N devices are visible (in a child process), starts N fresh rank
+processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* on 127.0.0.1), and exits
+with the first failing rank's code.  Every rank checks the world size and that
+its device is distinct from the others'.
 
-  value       particle-updates/s over all ranks = N_gpus · particles · K / t,
-              t = max over ranks of the timed K steps (barrier + device sync
-              on both sides; inputs resident in HBM)
-  roofline    the dominant kernel's algorithmic HBM bytes per launch ÷ its
-              average duration, measured with HIP events on the engine's
-              stream over the timed region; peak 8 TB/s (MI355X HBM3E)
-  cpu_baseline the keyed CPU oracle (single thread) on a bounded sample of
-              the same workload, rank 0 at N = 1 only
+Window.  After the keyed placement: W warm-up steps, a timed K-step window
+from the fresh placement (ms_per_step_fresh), E untimed evolution steps
+toward the bond-rich steady state the reference simulates for 2e7 steps, W
+warm-up steps with every kernel bracketed (per-kernel breakdown, dominant
+kernel), then THE timed window of exactly K steps (barrier + device sync on
+both sides, max over ranks) that `value` and `ms_per_step` report.
+
+Rank 0 prints ONE JSON line:
+  value        particle-updates/s over all ranks = N_gpus · particles · K / t
+  roofline     the dominant kernel's algorithmic HBM bytes per launch ÷ its
+               average duration (HIP events on the engine's stream over the
+               timed region); peak 8 TB/s (MI355X HBM3E)
+  cpu_baseline the keyed CPU oracle, one pinned core, on a bounded sample of
+               the same state (rank 0 at N = 1 only), plus an ensemble of one
+               oracle per core and the C1 link to the unmodified reference
 """
 from __future__ import annotations
 
@@ -22,33 +34,35 @@ import argparse
 import importlib
 import json
 import os
+import socket
+import subprocess
 import sys
+import tempfile
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 PKG = "kmc-with-a-diffusion-reaction-algorithm_amd"
-engine = importlib.import_module(PKG + ".engine")
 workloads = importlib.import_module(PKG + ".workloads")
-ensemble = importlib.import_module(PKG + ".ensemble")
 
 TIMING_EVERY = 8
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+METRIC = "KMC particle-updates/sec (and steps/sec) at 1e6 particles, 1/2/4/8 MI355X"
+MAX_CPU_WORKERS = 16  # the GPU box's CPU share for one GPU
 
 
 def kernel_bytes(name: str, n_a: int, n_b: int):
-    """Algorithmic HBM bytes per launch (DESIGN.md §roofline)."""
+    """Algorithmic HBM bytes per launch (DESIGN.md §5)."""
     n = n_a + n_b
     models = {
         # read R (16 receptor / 8 ligand beads × xyz × 8 B), write R_new, unit
         # kind; the record counts it also takes write one rank pair per protein
         "k_propose": 768 * n_a + 384 * n_b + n + 8 * n,
-        # every record once (float4 + id); candidate writes are data-dependent
+        # every record once (float4 + id)
         "k_col_scan": 2 * n * 24,
         # old + new reference points (x, y, zlo, zhi) + receptor site, record
         # write (pos, id, site), owner, cell cursor
         "k_rec_scatter": 2 * n * 32 + 2 * n_a * 16 + 2 * n * 32 + 4 * n + 2 * n * 8,
-        "k_rec_count": 2 * n * 32 + 2 * n * 4 + 48 * n_a + 48 * n_b,
         # every record once (float4 + id + site) + final flags
         "k_rxn_scan": 2 * n * 32 + n,
         "k_commit": 8 * n,
@@ -63,7 +77,7 @@ TRAFFIC_JSON = "profiles/traffic_C3.json"
 
 def pmc_traffic(kernel: str, workload: str):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
-    (FETCH_SIZE x2 + WRITE_SIZE, tools/pmc_traffic.py) of this same bench
+    (FETCH_SIZE + WRITE_SIZE, tools/pmc_traffic.py) of this same bench
     command; None when no profile of this workload is committed."""
     path = os.path.join(REPO, TRAFFIC_JSON)
     if workload != "C3" or not os.path.exists(path):
@@ -77,29 +91,126 @@ def kernel_trace_name(name: str) -> str:
     return {"k_rxn_scan": "k_rxn_scan_tile"}.get(name, name)
 
 
-def main():
+def parse(argv):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--workload", default="C3")
+    ap.add_argument("--workload", default="C3", choices=sorted(workloads.WORKLOADS))
+    ap.add_argument("--evolve", type=int, default=None,
+                    help="untimed steps before the timed window (default: the workload's, C3 20000)")
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--cpu-baseline-steps", type=int, default=4)
+    ap.add_argument("--cpu-baseline-steps", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-fresh-window", action="store_true")
     ap.add_argument("--profile", action="store_true", help="print the per-kernel breakdown to stderr")
-    args = ap.parse_args()
+    ap.add_argument("--launcher-check", action="store_true",
+                    help="ranks rendezvous over gloo and report who they are; no GPU work (launcher test)")
+    return ap.parse_args(argv)
 
+
+# ---------------------------------------------------------------- launcher
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def visible_devices() -> int:
+    """GPU count, asked in a child process so this launcher never touches HIP."""
+    r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                       capture_output=True, text=True)
+    try:
+        return int(r.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        return 0
+
+
+def launch(args, argv) -> int:
+    n = args.gpus
+    if not args.launcher_check:
+        ndev = visible_devices()
+        if ndev < n:
+            print(f"bench.py: --gpus {n} needs {n} visible GPUs, found {ndev}; refusing to measure fewer",
+                  file=sys.stderr, flush=True)
+            return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    alive = set(range(n))
+    while alive:
+        for r in sorted(alive):
+            c = procs[r].poll()
+            if c is None:
+                continue
+            alive.discard(r)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 1
+                print(f"bench.py: rank {r} exited with {c}; stopping the other ranks", file=sys.stderr, flush=True)
+                for q in alive:
+                    procs[q].terminate()
+        time.sleep(0.1)
+    return rc
+
+
+def launcher_check(rank: int, world: int, local: int):
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo")
+    assert dist.get_world_size() == world
+    who = [None] * world
+    dist.all_gather_object(who, {"rank": rank, "local_rank": local, "pid": os.getpid()})
+    if rank == 0:
+        print(json.dumps({"launcher_check": True, "world": world, "ranks": who}), flush=True)
+    dist.destroy_process_group()
+
+
+# ---------------------------------------------------------------- one rank
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch(args, argv))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.launcher_check:
+        launcher_check(rank, world, local)
+        return
+    run_rank(args, rank, world, local)
+
+
+def run_rank(args, rank: int, world: int, local: int):
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    engine = importlib.import_module(PKG + ".engine")
+    ensemble = importlib.import_module(PKG + ".ensemble")
+    # a diagnostic library (KMC_DIAG=1 KMC_LIB_PATH=..., capi.py) is named in the line
+    library = os.path.relpath(engine.load_library()._name, REPO)
+
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if dist.get_world_size() != world:
+            sys.exit(f"bench.py: process group has {dist.get_world_size()} ranks, expected {world}")
+        props = torch.cuda.get_device_properties(local)
+        me = str(getattr(props, "uuid", "")) or f"{props.name}:{local}"
+        devs = [None] * world
+        dist.all_gather_object(devs, me)
+        if len(set(devs)) != world:
+            sys.exit(f"bench.py: ranks share a device: {devs}")
     dev = torch.device("cuda", local)
 
+    w = workloads.WORKLOADS[args.workload]
+    evolve = w["evolve"] if args.evolve is None else args.evolve
     p = workloads.params(args.workload, seed=args.seed, replica=rank)
     n = p.n_a + p.n_b
     sim = engine.Simulation(p, device=local)
@@ -107,9 +218,48 @@ def main():
     sim.init_random()
     t_init = time.perf_counter() - t0
 
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    def timed(k):
+        barrier()
+        t = time.perf_counter()
+        obs = sim.step(k)
+        red = ensemble.reduce(obs, device=dev)
+        barrier()
+        return time.perf_counter() - t, red
+
+    def max_over_ranks(x):
+        if world == 1:
+            return x, [x]
+        allx = [None] * world
+        dist.all_gather_object(allx, x)
+        return max(allx), allx
+
+    # fresh placement window (bonds ~0: the early transient)
+    fresh_ms = None
+    if not args.no_fresh_window:
+        if args.warmup:
+            sim.step(args.warmup)
+        dt_f, _ = timed(args.steps)
+        fresh_ms = max_over_ranks(dt_f)[0] / args.steps * 1e3
+    # evolution toward the steady state (untimed)
+    t0 = time.perf_counter()
+    chunk = 5000
+    done = 0
+    while done < evolve:
+        k = min(chunk, evolve - done)
+        ob = sim.step(k)
+        done += k
+        if rank == 0:
+            print(f"bench: evolved {done}/{evolve} steps, bond_num {int(ob[-1]['bond_num'])}", file=sys.stderr,
+                  flush=True)
+    t_evolve = time.perf_counter() - t0
+
     # warm-up with every kernel bracketed: find the dominant kernel
-    names = engine.kernel_names()
-    sim.set_timing(names)
+    sim.set_timing(engine.kernel_names())
     if args.warmup:
         sim.step(args.warmup)
     kt = sim.kernel_times()
@@ -118,22 +268,8 @@ def main():
     # timed region: only the dominant kernel is bracketed, in every 8th step
     # (an event pair adds a few microseconds of queue time to its step)
     sim.set_timing([dom], every=TIMING_EVERY)
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-
-    barrier()
-    t0 = time.perf_counter()
-    obs = sim.step(args.steps)
-    sums, maxima, cluster = ensemble.reduce(obs, device=dev)
-    barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+    dt_local, (sums, maxima, cluster) = timed(args.steps)
+    dt, per_rank = max_over_ranks(dt_local)
 
     total_ms, launches = sim.kernel_times().get(dom, (0.0, 0))
     avg_s = total_ms / 1e3 / max(launches, 1)
@@ -145,15 +281,16 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(p, sim, args.cpu_baseline_steps)
+        steps = args.cpu_baseline_steps or w["cpu_sample_steps"]
+        cpu = cpu_baseline(args.workload, args.seed, sim, steps, w.get("cpu_ensemble_max", MAX_CPU_WORKERS))
 
     if args.profile and rank == 0:
-        print(json.dumps({"init_s": round(t_init, 3), "per_launch_ms": breakdown}), file=sys.stderr)
+        print(json.dumps({"init_s": round(t_init, 3), "evolve_s": round(t_evolve, 3), "per_launch_ms": breakdown}),
+              file=sys.stderr)
 
     if rank == 0:
-        w = workloads.WORKLOADS[args.workload]
         line = {
-            "metric": "KMC particle-updates/sec (and steps/sec) at 1e6 particles, 1/2/4/8 MI355X",
+            "metric": METRIC,
             "value": world * n * args.steps / dt,
             "unit": "particle-updates/s",
             "n_gpus": world,
@@ -173,7 +310,15 @@ def main():
                 "n_ligands": p.n_b,
                 "box_A": [p.box_x, p.box_y, p.box_z],
                 "parallelism": f"replicas x{world} (independent trajectories, RCCL all-reduce of observables)",
+                "evolve_steps": evolve,
+                "timed_from_step": sim.current_step - args.steps,
+                "ms_per_step_fresh": fresh_ms,
+                "per_rank_ms_per_step": [x / args.steps * 1e3 for x in per_rank],
+                "efficiency_vs_rank0": per_rank[0] / dt,
                 "final_bond_num_ensemble": int(sums[-1, 3]),
+                "final_rl_ensemble": int(sums[-1, 0]),
+                "max_complex_ensemble": int(maxima[-1, 0]),
+                "mean_cluster_size_ensemble": float(cluster[-1]),
             },
             "roofline": {
                 "bound": "hbm",
@@ -190,6 +335,7 @@ def main():
                 "step_frac": step_b / (ms_per_step / 1e3) / 1e9 / HBM_PEAK_GBS,
             },
             "cpu_baseline": cpu,
+            "library": library,
         }
         print(json.dumps(line), flush=True)
     sim.close()
@@ -197,24 +343,71 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(p, sim, steps: int):
-    """Keyed CPU oracle, one thread, a bounded sample of the same workload."""
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import oracle as O
+# ---------------------------------------------------------------- CPU baseline
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return ""
 
-    st = sim.get_state()
-    o = O.Oracle(p, rng_mode=O.RNG_KEYED, nbmode=O.NB_CELLS)
-    o.set_state(st)
-    t0 = time.perf_counter()
-    o.step(steps, want_hashes=False)
-    dt = time.perf_counter() - t0
-    n = p.n_a + p.n_b
+
+def _workers(jobs):
+    """Run oracle/cpu_worker.py jobs concurrently (fresh processes, no GPU);
+    returns their JSON results."""
+    script = os.path.join(REPO, "oracle", "cpu_worker.py")
+    procs = [subprocess.Popen([sys.executable, script, *j], stdout=subprocess.PIPE, text=True) for j in jobs]
+    out = []
+    for pr in procs:
+        so, _ = pr.communicate()
+        if pr.returncode != 0:
+            raise RuntimeError(f"cpu_worker failed ({pr.returncode})")
+        out.append(json.loads(so.strip().splitlines()[-1]))
+    return out
+
+
+def cpu_baseline(workload: str, seed: int, sim, steps: int, ens_max: int):
+    """Keyed CPU oracle (oracle/cpu_worker.py), each worker pinned to one core,
+    on the exact state the GPU run ended in; plus one worker per core
+    (ensemble) and the C1 conversion to the unmodified reference."""
+    cores = sorted(os.sched_getaffinity(0))
+    nens = min(len(cores), MAX_CPU_WORKERS, ens_max)
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "state.kmc")
+        sim.save_state(path)
+        base = ["--workload", workload, "--seed", str(seed), "--state", path, "--steps", str(steps)]
+        single = _workers([base + ["--core", str(cores[0])]])[0]
+        ens = _workers([base + ["--core", str(c)] for c in cores[:nens]]) if nens > 1 else [single]
+    c1_steps = 2000
+    c1 = _workers([["--workload", "C1", "--seed", "1", "--steps", str(c1_steps), "--core", str(cores[0])]])[0]
+    link = None
+    lpath = os.path.join(REPO, "profiles", "cpu_link_C1.json")
+    if os.path.exists(lpath):
+        L = json.load(open(lpath))
+        ratio = L["ratio_reference_over_oracle_cells"]
+        link = {
+            "oracle_C1_steps_per_s_here": c1["steps_per_s"],
+            "ratio_reference_over_oracle": ratio,
+            "ratio_source": "profiles/cpu_link_C1.json (tools/cpu_link.py; reference C1 rate from BASELINE.md)",
+            "reference_equiv_C1_steps_per_s": c1["steps_per_s"] * ratio,
+            "reference_equiv_C1_particle_updates_per_s": c1["steps_per_s"] * ratio * 2000,
+        }
     return {
-        "value": n * steps / dt,
+        "value": single["particle_updates_per_s"],
         "unit": "particle-updates/s",
         "cores": 1,
         "kind": "port",
-        "sample": f"{steps} steps of the same workload and state on the keyed oracle (cell-list mode), 1 thread",
+        "sample": f"{steps} steps of the same workload from the state the GPU run ended in, keyed oracle "
+                  f"(cell-list mode), one pinned core",
+        "host_cores": os.cpu_count(),
+        "host_cores_usable": len(cores),
+        "host_cpu": _cpu_model(),
+        "ensemble": {"value": sum(e["particle_updates_per_s"] for e in ens), "processes": len(ens),
+                     "unit": "particle-updates/s",
+                     "sample": f"one oracle process per usable core (at most {nens}), each pinned, same sample"},
+        "reference_link": link,
     }
 
 

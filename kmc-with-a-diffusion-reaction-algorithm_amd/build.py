@@ -7,6 +7,7 @@ contraction: results must match the sequential oracle bit for bit).
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -16,6 +17,7 @@ CSRC = os.path.join(HERE, "csrc")
 LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libkmc.so")
 RUN = os.path.join(LIB_DIR, "kmc_run")
+STAMP = os.path.join(LIB_DIR, ".build_stamp")  # content hash of the inputs of the current build
 SOURCES = ["kmc_engine.hip", "kmc_io.cpp"]
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
@@ -39,11 +41,23 @@ def _inputs():
     return files
 
 
+def source_hash() -> str:
+    """sha256 over every source file and the compiler flags: a build is reused only if it was made from exactly these inputs
+    (modification times are not trusted: a checkout or a copy resets them)."""
+    h = hashlib.sha256()
+    for f in sorted(_inputs()):
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    h.update(" ".join(FLAGS + os.environ.get("KMC_EXTRA_FLAGS", "").split()).encode())
+    return h.hexdigest()
+
+
 def stale() -> bool:
-    if not os.path.exists(LIB) or not os.path.exists(RUN):
+    if not (os.path.exists(LIB) and os.path.exists(RUN) and os.path.exists(STAMP)):
         return True
-    t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(f) > t for f in _inputs())
+    with open(STAMP) as f:
+        return f.read().strip() != source_hash()
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
@@ -51,6 +65,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
         return LIB
     _build_lib(verbose)
     _build_driver(verbose)
+    with open(STAMP, "w") as f:
+        f.write(source_hash() + "\n")
     return LIB
 
 

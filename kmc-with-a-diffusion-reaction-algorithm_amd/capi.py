@@ -1,7 +1,7 @@
 """ctypes mirror of include/kmc.h (the C-ABI of libkmc).
 
 Struct layouts here must match include/kmc.h field for field; the
-`tests/test_capi.py` CPU test checks sizes/offsets against the compiled
+`tests/test_host.py::test_ctypes_layouts_match_header` CPU test checks sizes/offsets against the compiled
 library.  Nothing in this module computes anything: it only marshals host
 buffers (numpy arrays) across the C boundary.
 """
@@ -13,7 +13,12 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# KMC_LIB_PATH: diagnostic builds only (e.g. the -DKMC_STAMPS timing build)
+# KMC_LIB_PATH: diagnostic builds only (e.g. the -DKMC_STAMPS timing build, the
+# A/B variants of tools/build_variants.py).  It is honoured only together with
+# KMC_DIAG=1, so a stray variable cannot make tests or benchmarks load a
+# library other than the in-tree build.
+if os.environ.get("KMC_LIB_PATH") and os.environ.get("KMC_DIAG") != "1":
+    raise RuntimeError("KMC_LIB_PATH is set without KMC_DIAG=1: refusing to load a non-default libkmc")
 LIB_PATH = os.environ.get("KMC_LIB_PATH") or os.path.join(HERE, "lib", "libkmc.so")
 
 KMC_OK = 0

@@ -39,7 +39,7 @@ struct Ctl {
   uint32_t step;          // mc_time_step being simulated
   uint32_t obs_idx;       // record index within the current kmc_step call
   uint32_t err;           // error bits (ERR_*)
-  uint32_t pad0;
+  uint32_t err_step;      // first step whose kernels raised an error bit (k_finalize), 0 = none
   // per-step work-list counters
   uint32_t n_overflow;    // ligands whose BFS overflowed the register queue
   uint32_t cx_cursor;     // members[] allocation cursor
@@ -57,7 +57,7 @@ struct Ctl {
 };
 
 enum : uint32_t {
-  ERR_EDGES = 1u,       // reaction edge buffer full
+  ERR_EDGES = 1u,       // an output list / reaction edge buffer full (kmc_step grows them and replays)
   ERR_GEOMETRY = 2u,    // rigid-body extent bound violated
   ERR_RESOLVE = 4u,     // collision resolution did not converge
   ERR_ALIGN = 8u,       // alignment repeat guard

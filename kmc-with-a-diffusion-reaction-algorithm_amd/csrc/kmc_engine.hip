@@ -37,13 +37,21 @@ struct kmc_sim {
   hipStream_t stream = nullptr;
   int64_t step_done = 0;
   std::string err;
-  int ncell = 0, nscan_blocks = 0;
+  int ncell = 0;
   bool have_state = false;
   std::vector<void*> allocs;
   kmc_obs_dev* obs_buf = nullptr;
   int64_t obs_cap = 0;
   Ctl* ctl_host = nullptr;
   bool poison = false;
+  // output-list capacities: 2^grow times the initial sizes; kmc_step doubles
+  // them and replays the chunk when a list overflows (ERR_EDGES)
+  int grow = 0;
+  // chunk snapshot for the replay: R, state rows, slot maps, control block
+  double *snap_a = nullptr, *snap_b = nullptr;
+  int32_t *snap_ai = nullptr, *snap_bi = nullptr, *snap_id = nullptr, *snap_slot = nullptr;
+  Ctl* snap_ctl = nullptr;
+  int64_t n_replays = 0;
   bool debug_counts = false;  // KMC_DEBUG_COUNTS=1: print the last step's work counts per kmc_step chunk
   // slot order (kmc_kernels.hip §slot order): scratch of the re-sort
   int64_t resort_every = 100, since_resort = 0;
@@ -94,6 +102,64 @@ int dalloc(kmc_sim* s, T** p, size_t n) {
   return KMC_OK;
 }
 
+uint32_t pow2(uint32_t n) {
+  uint32_t p = 1;
+  while (p < n) p <<= 1;
+  return p;
+}
+
+template <typename T>
+void dfree(kmc_sim* s, T*& p) {
+  if (!p) return;
+  auto it = std::find(s->allocs.begin(), s->allocs.end(), (void*)p);
+  if (it != s->allocs.end()) s->allocs.erase(it);
+  (void)hipFree((void*)p);
+  p = nullptr;
+}
+
+// The sharded output lists and the reaction-edge buffers, sized for 2^grow
+// times the defaults (grow < 0 only to test the replay: KMC_DEBUG_CAP_SHIFT).
+// Defaults: collision candidates ~1 per proposal at the benchmark densities,
+// every pair of records for small dense systems; per-shard capacity is the
+// total / NSHARD, but at least 64 Ki entries (a small dense system puts all of
+// its entries into the few shards of its few tiles).
+int alloc_lists(kmc_sim* s) {
+  Dev& d = s->d;
+  const uint64_t N = (uint64_t)s->K.N;
+  auto scale = [&](uint64_t v) {
+    return std::max<uint64_t>(64, s->grow >= 0 ? v << s->grow : v >> -s->grow);
+  };
+  dfree(s, d.cand.data);
+  dfree(s, d.conf.data);
+  dfree(s, d.plist.data);
+  dfree(s, d.rej.data);
+  dfree(s, d.pairs.data);
+  dfree(s, d.rl_keys);
+  dfree(s, d.cis_keys);
+  dfree(s, d.ent);
+  dfree(s, d.gi32);
+  uint32_t cap = (uint32_t)scale(pow2(std::max<uint32_t>(4096, std::min<uint32_t>(1u << 20, (uint32_t)N / 8 + 1))));
+  d.cap_edges = pow2(cap);
+  int rc = KMC_OK;
+  auto mk = [&](SList& l, uint64_t total, int which) {
+    total = scale(total);
+    l.cap = (uint32_t)std::max<uint64_t>((total + NSHARD - 1) / NSHARD, std::min<uint64_t>(total, scale(1u << 16)));
+    l.cnt = d.shard_cnt + which * NSHARD;
+    return dalloc(s, &l.data, (size_t)l.cap * NSHARD);
+  };
+  const uint64_t cand = std::max<uint64_t>(N, std::min<uint64_t>(4ull * N * N, 1ull << 22));
+  rc |= mk(d.cand, cand, 0);
+  rc |= mk(d.conf, cand, 1);
+  rc |= mk(d.plist, N, 2);
+  rc |= mk(d.rej, N, 3);
+  rc |= mk(d.pairs, std::max<uint64_t>(N, 1u << 16), 4);
+  rc |= dalloc(s, &d.rl_keys, d.cap_edges);
+  rc |= dalloc(s, &d.cis_keys, d.cap_edges);
+  rc |= dalloc(s, &d.ent, (size_t)2 * d.cap_edges);
+  rc |= dalloc(s, &d.gi32, (size_t)6 * d.cap_edges);
+  return rc;
+}
+
 // smallest T with sqrt(T) >= c, so that  sqrt(s) < c  <=>  s < T  (exact)
 double sqrt_threshold(double c) {
   double t = c * c;
@@ -102,11 +168,6 @@ double sqrt_threshold(double c) {
   return t;
 }
 
-uint32_t pow2(uint32_t n) {
-  uint32_t p = 1;
-  while (p < n) p <<= 1;
-  return p;
-}
 
 }  // namespace
 
@@ -193,12 +254,9 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   K.key = kmcr::make_key(p->seed, p->replica);
 
   s->ncell = 2 * K.ncx * K.ncy;  // (row, kind, column) record cells
-  s->nscan_blocks = (s->ncell + SCAN_T * SCAN_PER - 1) / (SCAN_T * SCAN_PER);
   Dev& d = s->d;
   d.cur.NA = d.nxt.NA = NA;
   d.cur.NB = d.nxt.NB = NB;
-  uint32_t cap = pow2(std::max<uint32_t>(4096, std::min<uint32_t>(1u << 20, (uint32_t)N / 8 + 1)));
-  d.cap_edges = cap;
   int rc = KMC_OK;
   rc |= dalloc(s, &d.cur.a, (size_t)48 * NA);
   rc |= dalloc(s, &d.nxt.a, (size_t)48 * NA);
@@ -232,33 +290,15 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   rc |= dalloc(s, &d.cell_cnt_alt, s->ncell + 1);
   d.ncnt = s->ncell + 1;
   rc |= dalloc(s, &d.cell_start, s->ncell + 1);
-  rc |= dalloc(s, &d.block_sums, s->nscan_blocks);
   rc |= dalloc(s, &d.rec, (size_t)2 * N);
-  // collision candidates: ~1 per proposal at the benchmark densities; every
-  // pair of records for small dense systems
-  // sharded output lists (kmc_kernels.hip §SList): per-shard capacity is the
-  // total / NSHARD, but at least 64 Ki entries (a small dense system puts all
-  // of its entries into the few shards of its few tiles)
   rc |= dalloc(s, &d.shard_cnt, (size_t)5 * NSHARD);
   {
-    auto mk = [&](SList& l, uint64_t total, int which) {
-      l.cap = (uint32_t)std::max<uint64_t>((total + NSHARD - 1) / NSHARD, std::min<uint64_t>(total, 1u << 16));
-      l.cnt = d.shard_cnt + which * NSHARD;
-      return dalloc(s, &l.data, (size_t)l.cap * NSHARD);
-    };
-    const uint64_t cand = std::max<uint64_t>(N, std::min<uint64_t>(4ull * N * N, 1ull << 22));
-    rc |= mk(d.cand, cand, 0);
-    rc |= mk(d.conf, cand, 1);
-    rc |= mk(d.plist, N, 2);
-    rc |= mk(d.rej, N, 3);
-    rc |= mk(d.pairs, std::max<uint64_t>(N, 1u << 16), 4);
+    const char* cs = getenv("KMC_DEBUG_CAP_SHIFT");  // debug: start with lists 2^k times too small
+    s->grow = cs && *cs ? -std::max(0, std::min(20, atoi(cs))) : 0;
   }
+  rc |= alloc_lists(s);
   rc |= dalloc(s, &d.rank, N);
   rc |= dalloc(s, &d.obs_part, (size_t)8 * ((N + 255) / 256));
-  rc |= dalloc(s, &d.rl_keys, cap);
-  rc |= dalloc(s, &d.cis_keys, cap);
-  rc |= dalloc(s, &d.ent, (size_t)2 * cap);
-  rc |= dalloc(s, &d.gi32, (size_t)6 * cap);
   rc |= dalloc(s, &d.bfs_queue, N);
   rc |= dalloc(s, &d.vtag, N);
   rc |= dalloc(s, &d.ctl, 1);
@@ -395,6 +435,54 @@ static int resort(kmc_sim* s) {
   return hipGetLastError() == hipSuccess ? KMC_OK : fail(s, KMC_ERR_HIP, "resort launch");
 }
 
+// Every array that carries a step / round tag or a per-step count: a state
+// (re)loaded at an earlier step must not meet tags of a later one.
+static int clear_step_tags(kmc_sim* s) {
+  Dev& d = s->d;
+  const size_t N = (size_t)s->K.N;
+  hipStream_t st = s->stream;
+  HIPCHK(s, hipMemsetAsync(d.ustate, 0, sizeof(uint32_t) * N, st));
+  HIPCHK(s, hipMemsetAsync(d.moved, 0, sizeof(uint32_t) * N, st));
+  HIPCHK(s, hipMemsetAsync(d.pend, 0, sizeof(uint32_t) * N, st));
+  HIPCHK(s, hipMemsetAsync(d.vtag, 0, sizeof(uint32_t) * N, st));
+  HIPCHK(s, hipMemsetAsync(d.cell_cnt, 0, sizeof(int32_t) * (size_t)d.ncnt, st));
+  HIPCHK(s, hipMemsetAsync(d.cell_cnt_alt, 0, sizeof(int32_t) * (size_t)d.ncnt, st));
+  HIPCHK(s, hipMemsetAsync(d.shard_cnt, 0, sizeof(uint32_t) * 5 * NSHARD, st));
+  return KMC_OK;
+}
+
+// Chunk snapshot (kmc_step): everything a step reads from the previous one —
+// R (device layout), state rows, slot maps, control block.  Everything else
+// is rewritten within a step or is a tag cleared by clear_step_tags.
+static int snapshot(kmc_sim* s, bool restore) {
+  Dev& d = s->d;
+  const size_t NA = (size_t)s->K.NA, NB = (size_t)s->K.NB, N = NA + NB;
+  hipStream_t st = s->stream;
+  if (!s->snap_ctl) {
+    int rc = KMC_OK;
+    rc |= dalloc(s, &s->snap_a, 48 * NA);
+    rc |= dalloc(s, &s->snap_b, 24 * NB);
+    rc |= dalloc(s, &s->snap_ai, 5 * NA);
+    rc |= dalloc(s, &s->snap_bi, 8 * NB);
+    rc |= dalloc(s, &s->snap_id, N);
+    rc |= dalloc(s, &s->snap_slot, N);
+    rc |= dalloc(s, &s->snap_ctl, 1);
+    if (rc != KMC_OK) return rc;
+  }
+  auto cp = [&](void* live, void* snap, size_t bytes) {
+    return restore ? hipMemcpyAsync(live, snap, bytes, hipMemcpyDeviceToDevice, st)
+                   : hipMemcpyAsync(snap, live, bytes, hipMemcpyDeviceToDevice, st);
+  };
+  HIPCHK(s, cp(d.cur.a, s->snap_a, sizeof(double) * 48 * NA));
+  HIPCHK(s, cp(d.cur.b, s->snap_b, sizeof(double) * 24 * NB));
+  HIPCHK(s, cp(d.a_int, s->snap_ai, sizeof(int32_t) * 5 * NA));
+  HIPCHK(s, cp(d.b_int, s->snap_bi, sizeof(int32_t) * 8 * NB));
+  HIPCHK(s, cp(d.id_of, s->snap_id, sizeof(int32_t) * N));
+  HIPCHK(s, cp(d.slot_of, s->snap_slot, sizeof(int32_t) * N));
+  HIPCHK(s, cp(d.ctl, s->snap_ctl, sizeof(Ctl)));
+  return restore ? clear_step_tags(s) : KMC_OK;
+}
+
 int kmc_set_state(kmc_sim* s, const kmc_state_view* v) {
   if (!s || !v) return KMC_ERR_ARG;
   int rc = kmch_host::validate(&s->p, v, &s->err);
@@ -420,8 +508,8 @@ int kmc_set_state(kmc_sim* s, const kmc_state_view* v) {
   c.off_mono = v->counters[3] - mono;
   c.maxc = v->counters[4];
   HIPCHK(s, hipMemcpy(d.ctl, &c, sizeof c, hipMemcpyHostToDevice));
-  HIPCHK(s, hipMemset(d.ustate, 0, sizeof(uint32_t) * (size_t)(NA + NB)));
-  HIPCHK(s, hipMemset(d.moved, 0, sizeof(uint32_t) * (size_t)(NA + NB)));
+  rc = clear_step_tags(s);
+  if (rc != KMC_OK) return rc;
   // reference order = identity slots, then the spatial sort
   k_iota<<<(NA + NB + 255) / 256, 256, 0, s->stream>>>(d.id_of, d.slot_of, NA + NB);
   if (NA > 0)
@@ -617,6 +705,38 @@ static int launch_step(kmc_sim* s, bool re_sort) {
   return KMC_OK;
 }
 
+// Launch n steps from the current state; device obs records land in obs_buf.
+// Returns after the stream has drained, with the control block in ctl_host.
+static int run_chunk(kmc_sim* s, int64_t n) {
+  uint32_t zero = 0;
+  HIPCHK(s, hipMemcpyAsync(&s->d.ctl->obs_idx, &zero, sizeof zero, hipMemcpyHostToDevice, s->stream));
+  for (int64_t k = 0; k < n; ++k) {
+    const bool rs = s->resort_every > 0 && ++s->since_resort >= s->resort_every;
+    if (rs) s->since_resort = 0;
+    // unit-state tags are (step mod 2^30): clear them when the tag wraps
+    if (((s->step_done + k + 1) & 0x3fffffff) == 0)
+      HIPCHK(s, hipMemsetAsync(s->d.ustate, 0, sizeof(uint32_t) * (size_t)s->K.N, s->stream));
+    int rc = launch_step(s, rs);
+    if (rc != KMC_OK) return rc;
+  }
+  HIPCHK(s, hipGetLastError());
+  HIPCHK(s, hipMemcpyAsync(s->ctl_host, s->d.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, s->stream));
+  HIPCHK(s, hipStreamSynchronize(s->stream));
+  if (s->tmask)
+    for (int slot = 0; slot < TRING; ++slot) harvest(s, slot);
+  return KMC_OK;
+}
+
+// Steps run in chunks of up to 4096 launched back to back; the device error
+// bits are read once per chunk.  Every chunk starts from a device snapshot of
+// its initial state, so a chunk that raised an error bit is undone:
+//  * an output list or edge buffer overflowed (ERR_EDGES): the lists are
+//    doubled and the chunk replayed — with keyed draws the replay is the same
+//    trajectory, so capacities never change results;
+//  * anything else (geometry bound, unresolved conflicts, members overflow):
+//    the steps before the failing one are replayed and kept, kmc_step returns
+//    the error, and the state and kmc_current_step() are those of the last
+//    good step.
 int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out) {
   if (!s) return KMC_ERR_ARG;
   if (!s->have_state) return fail(s, KMC_ERR_ARG, "no state: call kmc_init_random / kmc_load_cpt / kmc_set_state");
@@ -630,30 +750,48 @@ int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out) {
   }
   int64_t done = 0;
   while (done < nsteps) {
-    int64_t n = std::min(chunk, nsteps - done);
-    uint32_t zero = 0;
-    HIPCHK(s, hipMemcpyAsync(&s->d.ctl->obs_idx, &zero, sizeof zero, hipMemcpyHostToDevice, s->stream));
-    for (int64_t k = 0; k < n; ++k) {
-      const bool rs = s->resort_every > 0 && ++s->since_resort >= s->resort_every;
-      if (rs) s->since_resort = 0;
-      // unit-state tags are (step mod 2^30): clear them when the tag wraps
-      if (((s->step_done + k + 1) & 0x3fffffff) == 0)
-        HIPCHK(s, hipMemsetAsync(s->d.ustate, 0, sizeof(uint32_t) * (size_t)s->K.N, s->stream));
-      int rc = launch_step(s, rs);
+    const int64_t n = std::min(chunk, nsteps - done);
+    int rc = snapshot(s, false);
+    if (rc != KMC_OK) return rc;
+    const int64_t since0 = s->since_resort;
+    for (;;) {
+      rc = run_chunk(s, n);
       if (rc != KMC_OK) return rc;
+      const uint32_t err = s->ctl_host->err;
+      if (!err) break;
+      const int64_t bad = (int64_t)s->ctl_host->err_step;
+      rc = snapshot(s, true);
+      if (rc != KMC_OK) return rc;
+      s->since_resort = since0;
+      ++s->n_replays;
+      if (err == ERR_EDGES && s->grow < 6) {  // at most 64x the default lists
+        s->grow += 1;
+        if (alloc_lists(s) != KMC_OK) return fail(s, KMC_ERR_HIP, "growing the output lists failed");
+        continue;
+      }
+      // keep the steps before the failing one
+      const int64_t good = std::max<int64_t>(0, std::min<int64_t>(n, bad - (s->step_done + 1)));
+      if (good > 0) {
+        rc = run_chunk(s, good);
+        if (rc != KMC_OK) return rc;
+        if (out)
+          HIPCHK(s, hipMemcpy(out + done, s->obs_buf, sizeof(kmc_obs_dev) * good, hipMemcpyDeviceToHost));
+        s->step_done += good;
+      }
+      char m[200];
+      snprintf(m, sizeof m, "device error bits 0x%x at step %lld; state kept at step %lld", err, (long long)bad,
+               (long long)s->step_done);
+      const int code = (err & ERR_GEOMETRY) ? KMC_ERR_GEOMETRY : KMC_ERR_CAPACITY;
+      return fail(s, code, m);
     }
-    HIPCHK(s, hipGetLastError());
-    HIPCHK(s, hipMemcpyAsync(s->ctl_host, s->d.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, s->stream));
     if (out)
-      HIPCHK(s, hipMemcpyAsync(out + done, s->obs_buf, sizeof(kmc_obs_dev) * n, hipMemcpyDeviceToHost, s->stream));
-    HIPCHK(s, hipStreamSynchronize(s->stream));
-    if (s->tmask)
-      for (int slot = 0; slot < TRING; ++slot) harvest(s, slot);
+      HIPCHK(s, hipMemcpy(out + done, s->obs_buf, sizeof(kmc_obs_dev) * n, hipMemcpyDeviceToHost));
     s->step_done += n;
     if (s->debug_counts) {
       const uint32_t* l = s->ctl_host->last;
-      fprintf(stderr, "kmc step %lld: candidates %u conflicts %u pending-units %u rejected %u rxn-pairs %u rl-edges %u cis-edges %u bfs-overflow %u\n",
-              (long long)s->step_done, l[0], l[1], l[2], l[3], l[4], l[5], l[6], l[7]);
+      fprintf(stderr, "kmc step %lld: candidates %u conflicts %u pending-units %u rejected %u rxn-pairs %u rl-edges %u cis-edges %u bfs-overflow %u (list growth 2^%d, replays %lld)\n",
+              (long long)s->step_done, l[0], l[1], l[2], l[3], l[4], l[5], l[6], l[7], s->grow,
+              (long long)s->n_replays);
       const uint64_t* t = s->ctl_host->stamps;
       if (t[0] | t[8])
         fprintf(stderr, "kmc stamps col %llu %llu %llu %llu %llu %llu %llu %llu rxn %llu %llu %llu %llu %llu %llu %llu %llu\n",
@@ -661,13 +799,6 @@ int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out) {
                 (unsigned long long)t[4], (unsigned long long)t[5], (unsigned long long)t[6], (unsigned long long)t[7],
                 (unsigned long long)t[8], (unsigned long long)t[9], (unsigned long long)t[10], (unsigned long long)t[11],
                 (unsigned long long)t[12], (unsigned long long)t[13], (unsigned long long)t[14], (unsigned long long)t[15]);
-    }
-    uint32_t err = s->ctl_host->err;
-    if (err) {
-      char m[160];
-      snprintf(m, sizeof m, "device error bits 0x%x near step %lld", err, (long long)s->step_done);
-      int code = (err & ERR_GEOMETRY) ? KMC_ERR_GEOMETRY : KMC_ERR_CAPACITY;
-      return fail(s, code, m);
     }
     done += n;
   }

@@ -61,7 +61,6 @@ struct Dev {
   int32_t* cell_cnt_alt;  // [ncell+1] the next step's counts: zeroed by k_diss_observe, swapped after the step
   int ncnt;             // ncell+1
   int32_t* cell_start;  // [ncell+1]
-  int32_t* block_sums;  // [scan blocks]
   struct Rec* rec;      // [2N] cell-sorted records (old and proposed position of every protein)
   SList cand;           // collision candidates (proposal record, other record)
   SList conf;           // conflict entries (u, kq | isnew<<31)
@@ -1065,65 +1064,6 @@ __global__ void __launch_bounds__(256) k_propose(KParams P, Dev d) {
     return;
   }
   propose_one(P, d, ((int)blockIdx.x - P.cx_blocks) * blockDim.x + threadIdx.x);
-}
-
-// exclusive scan of cell_cnt[0..n) into cell_start[0..n]; 3 kernels
-#define SCAN_T 1024
-#define SCAN_PER 4
-__global__ void k_scan1(int32_t* in, int32_t* out, int32_t* sums, int n) {
-  __shared__ int32_t s[SCAN_T];
-  int base = (blockIdx.x * SCAN_T + threadIdx.x) * SCAN_PER;
-  int v[SCAN_PER];
-  int tot = 0;
-#pragma unroll
-  for (int q = 0; q < SCAN_PER; ++q) {
-    v[q] = base + q < n ? in[base + q] : 0;
-    if (base + q < n) in[base + q] = 0;  // counts start from zero next step
-    tot += v[q];
-  }
-  s[threadIdx.x] = tot;
-  __syncthreads();
-  for (int off = 1; off < SCAN_T; off <<= 1) {
-    int t = threadIdx.x >= off ? s[threadIdx.x - off] : 0;
-    __syncthreads();
-    s[threadIdx.x] += t;
-    __syncthreads();
-  }
-  int run = s[threadIdx.x] - tot;
-#pragma unroll
-  for (int q = 0; q < SCAN_PER; ++q) {
-    if (base + q < n) out[base + q] = run;
-    run += v[q];
-  }
-  if (threadIdx.x == SCAN_T - 1) sums[blockIdx.x] = s[SCAN_T - 1];
-}
-__global__ void k_scan2(int32_t* sums, int nb, int32_t* total_out) {
-  __shared__ int32_t s[SCAN_T];
-  int carry = 0;
-  for (int base = 0; base < nb; base += SCAN_T) {
-    int i = base + threadIdx.x;
-    int v = i < nb ? sums[i] : 0;
-    s[threadIdx.x] = v;
-    __syncthreads();
-    for (int off = 1; off < SCAN_T; off <<= 1) {
-      int t = threadIdx.x >= off ? s[threadIdx.x - off] : 0;
-      __syncthreads();
-      s[threadIdx.x] += t;
-      __syncthreads();
-    }
-    if (i < nb) sums[i] = carry + s[threadIdx.x] - v;
-    int blk = s[SCAN_T - 1];
-    __syncthreads();
-    carry += blk;
-  }
-  if (threadIdx.x == 0) *total_out = carry;
-}
-__global__ void k_scan3(int32_t* out, const int32_t* sums, int n) {
-  int base = (blockIdx.x * SCAN_T + threadIdx.x) * SCAN_PER;
-  int add = sums[blockIdx.x];
-#pragma unroll
-  for (int q = 0; q < SCAN_PER; ++q)
-    if (base + q < n) out[base + q] += add;
 }
 
 #define RID_PID 0x00ffffff
@@ -2419,6 +2359,7 @@ __global__ void __launch_bounds__(256) k_finalize(KParams P, Dev d, double time_
   o.tot_clu = tot_clu;
   o.reserved = 0;
   d.obs[obs_idx] = o;
+  if (c->err && c->err_step == 0) c->err_step = step;  // kmc_step replays up to here
   c->maxc = maxc;
   c->obs_idx = obs_idx + 1;
   c->step = step + 1;

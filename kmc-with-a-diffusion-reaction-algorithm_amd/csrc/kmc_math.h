@@ -13,7 +13,8 @@
 // -ffp-contract=off on both host and device (no FMA contraction).
 //
 // Accuracy: < 1 ulp over the arguments the simulation produces (|x| < 2^19·π/2
-// for sin/cos); checked against libm in tests/test_numerics.py.
+// for sin/cos); checked against libm in tests/test_oracle_modes.py
+// (test_portable_libm_within_one_ulp, test_portable_libm_exact_points).
 #pragma once
 #include <stdint.h>
 
@@ -36,7 +37,7 @@ KMC_HD double fabs_(double x) { return from_bits(bits(x) & 0x7fffffffffffffffull
 
 // IEEE-754 correctly rounded square root (sqrtsd on x86-64; on gfx950 the
 // compiler's f64 sqrt lowering is validated bit-for-bit in
-// tests/test_gpu_numerics.py).
+// tests/test_gpu_parity.py::test_device_math_bitexact).
 KMC_HD double sqrt_(double x) { return __builtin_sqrt(x); }
 
 // round-half-away-from-zero, exact (C99 round()).  main.cpp:597 uses round()

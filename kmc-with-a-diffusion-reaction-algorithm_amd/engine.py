@@ -243,6 +243,9 @@ class Simulation:
         """Advance n steps; returns the n bond.dat records (capi.OBS_DTYPE)."""
         if out is None:
             out = np.zeros(n, dtype=capi.OBS_DTYPE)
+        elif out.dtype != capi.OBS_DTYPE or not out.flags.c_contiguous or not out.flags.writeable or len(out) < n:
+            # kmc_step writes n records of sizeof(kmc_obs) through the pointer
+            raise ValueError(f"out must be a writeable C-contiguous capi.OBS_DTYPE array of length >= {n}")
         self._check(load_library().kmc_step(self._h, n, out.ctypes.data_as(C.c_void_p)))
         return out
 

@@ -20,14 +20,14 @@ def step_bytes(n_a: int, n_b: int) -> int:
 
 
 WORKLOADS = {
-    "C1": dict(n_a=1000, n_b=1000, L=5773.0, steps=10000,
+    "C1": dict(n_a=1000, n_b=1000, L=5773.0, steps=10000, evolve=0, cpu_sample_steps=2000,
                desc="1e3 receptors + 1e3 ligands, reference box 5773x5773x1000 A"),
-    "C2": dict(n_a=75000, n_b=25000, L=5773.0 * math.sqrt(100000 / 200), steps=100000,
+    "C2": dict(n_a=75000, n_b=25000, L=5773.0 * math.sqrt(100000 / 200), steps=100000, evolve=0, cpu_sample_steps=40,
                desc="1e5 particles (75000 A + 25000 B) at the reference density"),
-    "C3": dict(n_a=750000, n_b=250000, L=5773.0 * math.sqrt(1000000 / 2000), steps=None,
-               desc="1e6 particles (750000 A + 250000 B), dense box (10x area density)"),
-    "C5": dict(n_a=5000000, n_b=5000000, L=5773.0 * math.sqrt(5000000 / 1500), steps=None,
-               desc="1e7 particles (5e6 A + 5e6 B), high ligand concentration"),
+    "C3": dict(n_a=750000, n_b=250000, L=5773.0 * math.sqrt(1000000 / 2000), steps=None, evolve=20000,
+               cpu_sample_steps=4, desc="1e6 particles (750000 A + 250000 B), dense box (10x area density)"),
+    "C5": dict(n_a=5000000, n_b=5000000, L=5773.0 * math.sqrt(5000000 / 1500), steps=None, evolve=20000,
+               cpu_sample_steps=1, cpu_ensemble_max=4, desc="1e7 particles (5e6 A + 5e6 B), high ligand concentration"),
 }
 
 

@@ -24,7 +24,7 @@
 // Neighbour modes: 0 = brute force over all proteins (exactly the
 // reference's O(N^2) loops), 1 = a 130 Å xy cell list.  The cell list only
 // prunes pairs that cannot pass a distance test; loop order and therefore
-// results are unchanged (tests/test_oracle.py checks 0 ≡ 1).
+// results are unchanged (tests/test_oracle_modes.py::test_brute_equals_cells_* check 0 ≡ 1).
 //
 // Numerics: sin/cos/atan2/acos come from kmc_math.h (the same portable
 // fdlibm restatement the device code and the reference interposer use);

@@ -67,6 +67,7 @@ def lib():
         L.oracle_current_step.argtypes = [C.c_void_p]
         L.oracle_last_error.restype = C.c_char_p
         L.oracle_stats.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+        L.oracle_get_clusters.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.oracle_set_stream.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64]
         L.oracle_stream_clock.restype = C.c_uint64
         L.oracle_stream_clock.argtypes = [C.c_void_p]
@@ -135,6 +136,14 @@ class Oracle:
     @property
     def stream_position(self):
         return int(lib().oracle_stream_clock(self.h)), int(lib().oracle_rand_calls(self.h))
+
+    def clusters(self):
+        """BFS member rows of the last step (main.cpp:537 after the shuffles):
+        (row_len[n_b], members) in kmc_get_clusters' format."""
+        row = np.zeros(self.params.n_b, dtype=np.int32)
+        mem = np.zeros(self.params.n_a + self.params.n_b, dtype=np.int32)
+        lib().oracle_get_clusters(self.h, row.ctypes.data, mem.ctypes.data)
+        return row, mem[: int(row.sum())]
 
     def hash(self) -> int:
         return int(lib().oracle_hash(self.h))

@@ -19,7 +19,7 @@
 //     runs use that size and vary box, rates and step count instead.
 //  4. rand() (random_shuffle's source) is glibc's own algorithm restated with a
 //     call counter (kmc_glibc_rand.h, checked equal to glibc in
-//     tests/test_oracle.py) so a run can be resumed mid-trajectory.
+//     tests/test_oracle_modes.py::test_glibc_rand_restatement_equals_libc) so a run can be resumed mid-trajectory.
 //  5. A per-step trace: at the first clock read of step s (the committed
 //     state of step s-1 is still in R_x/R_y/R_z, protein_status, res_nei and
 //     the counters) one line is appended to $KMC_REF_TRACE:

@@ -55,8 +55,10 @@ SCENARIOS = {
         t0=4242,
         steps=20000,
         params=DENSE,
-        dump=[4999, 8000, 9999, 15000, 20000],
-        keep=[(0, 2000), (8000, 10000), (15000, 16000)],
+        # x999 dumps: the state one step before each output step, from which
+        # the cluster.log blocks (main.cpp:2291-2305) are regenerated
+        dump=[4999, 8000, 9999, 14999, 15000, 19999, 20000],
+        keep=[(0, 2000), (4999, 5000), (8000, 10000), (14999, 16000), (19999, 20000)],
         cpt_at=[5000, 10000, 15000, 20000],
     ),
     # resume from the reference's own position.cpt of "dense" at step 5000
@@ -65,8 +67,8 @@ SCENARIOS = {
         t0=99,
         steps=10000,
         params=DENSE,
-        dump=[5000, 10000],
-        keep=[(5000, 6500)],
+        dump=[5000, 9999, 10000],
+        keep=[(5000, 6500), (9999, 10000)],
         input_cpt=("dense", 5000),
         cpt_at=[10000],
     ),

@@ -55,3 +55,83 @@ def test_two_replica_allreduce(tmp_path):
     assert np.array_equal(got["m"], np.maximum(ma, mb))
     tp, tc = (sa + sb)[:, 4], (sa + sb)[:, 5]
     assert np.allclose(got["cluster"], np.where(tc > 0, tp / np.maximum(tc, 1), 0.0))
+
+
+# ---------------------------------------------------------------- bench launcher
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(REPO, "bench.py")
+
+
+def _bench(*args, env=None):
+    import subprocess
+    import sys
+
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    e.update(env or {})
+    return subprocess.run([sys.executable, BENCH, *args], capture_output=True, text=True, env=e, timeout=300)
+
+
+def test_bench_launcher_starts_n_ranks():
+    # bench.py --gpus 2 without torchrun: a GPU-free parent starts 2 rank
+    # processes that rendezvous (gloo here) with distinct ranks
+    import json
+
+    r = _bench("--gpus", "2", "--launcher-check")
+    assert r.returncode == 0, r.stderr
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["world"] == 2
+    assert sorted(x["rank"] for x in line["ranks"]) == [0, 1]
+    assert sorted(x["local_rank"] for x in line["ranks"]) == [0, 1]
+    assert len({x["pid"] for x in line["ranks"]}) == 2
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    r = _bench("--gpus", "64")
+    assert r.returncode != 0
+    assert "refusing" in r.stderr
+
+
+def test_bench_refuses_world_size_mismatch():
+    r = _bench("--gpus", "1", env={"WORLD_SIZE": "2"})
+    assert r.returncode != 0
+    assert "WORLD_SIZE" in r.stderr
+
+
+# ---------------------------------------------------------------- replicas on the GPU
+def _gpu_worker(rank, world, port, out, steps):
+    import torch.distributed as dist
+
+    engine = importlib.import_module(PKG + ".engine")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    p = params(seed=99, replica=rank, **DENSE)
+    with engine.Simulation(p, device=0) as sim:
+        sim.set_state(engine.host_init_random(p))
+        obs = sim.step(steps)
+    s, m, cluster = ensemble.reduce(obs)  # CPU tensors over gloo (two ranks share one GPU)
+    if rank == 0:
+        np.savez(out, s=s, m=m, cluster=cluster)
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_two_gpu_replicas_reduced_equal_oracle_sum(tmp_path):
+    # two replica trajectories through the HIP engine (one process each, same
+    # GPU); the all-reduced series equals the sum / max of two keyed-oracle runs
+    engine = importlib.import_module(PKG + ".engine")
+    steps = 400
+    out = str(tmp_path / "ens_gpu.npz")
+    mp.spawn(_gpu_worker, args=(2, _free_port(), out, steps), nprocs=2, join=True)
+    got = np.load(out)
+    ref = []
+    for r in range(2):
+        p = params(seed=99, replica=r, **DENSE)
+        o = O.Oracle(p)
+        o.set_state(engine.host_init_random(p))
+        ref.append(o.step(steps, want_hashes=False)[0])
+    assert not np.array_equal(ref[0], ref[1])
+    sa, ma = ensemble.pack(ref[0])
+    sb, mb = ensemble.pack(ref[1])
+    assert np.array_equal(got["s"], sa + sb)
+    assert np.array_equal(got["m"], np.maximum(ma, mb))
+    assert (sa + sb)[-1, 3] > 0, "the window should form bonds"

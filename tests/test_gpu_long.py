@@ -1,0 +1,36 @@
+"""C2 long-horizon bit-exactness (BASELINE.json config 2: "1e5 particles ...
+fixed seed — bit-exact state counts vs CPU").
+
+tests/golden/c2_long.npz holds the keyed CPU oracle's (cell-list mode) run of
+C2 (75 000 + 25 000 proteins, reference physics and density, seed 1) from the
+keyed placement: every step's bond.dat record (main.cpp:2251 columns + cluster
+sums) and the full-state hash every 100 steps, for 10 000 steps
+(tests/golden/make_c2_long.py, about an hour of CPU).  The GPU replays the
+whole window here in seconds."""
+import os
+
+import numpy as np
+import pytest
+
+from _kmc import GOLDEN, engine, workloads
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.timeout(600)
+def test_c2_long_horizon_matches_oracle_fixture():
+    g = np.load(os.path.join(GOLDEN, "c2_long.npz"), allow_pickle=False)
+    steps, every = int(g["steps"]), int(g["hash_every"])
+    p = workloads.params("C2", seed=int(g["seed"]))
+    sim = engine.Simulation(p)
+    sim.set_state(engine.host_init_random(p))
+    for c in range(steps // every):
+        obs = sim.step(every)
+        ref = g["obs"][c * every:(c + 1) * every]
+        if not np.array_equal(obs, ref):
+            s = int(np.flatnonzero(obs != ref)[0])
+            pytest.fail(f"step {c * every + s + 1}: gpu {obs[s]} oracle {ref[s]}")
+        h = engine.state_hash(p, sim.get_state())
+        assert h == int(g["hashes"][c]), f"state hash differs at step {(c + 1) * every}"
+    assert sim.current_step == steps
+    assert g["obs"][-1]["bond_num"] > 300

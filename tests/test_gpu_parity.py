@@ -198,3 +198,24 @@ def test_benchmark_workload_window(name, steps):
     obs_o, _ = o.step(steps, want_hashes=False)
     assert np.array_equal(obs, obs_o)
     assert engine.state_hash(p, sim.get_state()) == o.hash()
+
+
+def test_list_overflow_grow_and_replay(monkeypatch, capfd):
+    # every output list and edge buffer starts 2^10 times too small: chunks
+    # overflow, are undone from the device snapshot, the lists doubled and
+    # the chunk replayed — the trajectory must not change (kmc_step)
+    monkeypatch.setenv("KMC_DEBUG_CAP_SHIFT", "10")
+    monkeypatch.setenv("KMC_DEBUG_COUNTS", "1")
+    p = params(seed=37, **DENSE)
+    o = O.Oracle(p)
+    o.init_placement()
+    sim = engine.Simulation(p)
+    sim.set_state(o.get_state())
+    obs = np.concatenate([sim.step(700), sim.step(800)])
+    obs_o, _ = o.step(1500, want_hashes=False)
+    assert np.array_equal(obs, obs_o)
+    assert engine.state_hash(p, sim.get_state()) == o.hash()
+    assert sim.current_step == 1500
+    import re
+    replays = [int(x) for x in re.findall(r"replays (\d+)", capfd.readouterr().err)]
+    assert replays and replays[-1] > 0, "the lists never overflowed: the replay path was not exercised"

@@ -1,0 +1,70 @@
+"""Steady-state parity at the benchmark sizes.
+
+The reference simulates 2e7 steps; a fresh placement has no bonds.  Here the
+GPU evolves a benchmark configuration for thousands of steps (untimed, not
+checked step by step — too long for the CPU), then the exact state it reached
+(kmc_get_state, full precision) is handed to the keyed oracle (cell-list
+mode) and a window of steps is compared bit for bit: every bond.dat record
+and the full-state hash.  The oracle's event counters show which code paths
+the window exercised (complexes, lay-down, alignment, dissociations,
+collision rejections)."""
+import sys
+import time
+
+import numpy as np
+import pytest
+
+from _kmc import DENSE, O, engine, workloads
+
+pytestmark = pytest.mark.gpu
+
+RATES = {k: v for k, v in DENSE.items() if not k.startswith("box")}
+
+
+def _evolved_window(p, evolve, window):
+    sim = engine.Simulation(p)
+    sim.set_state(engine.host_init_random(p))
+    t = time.time()
+    done = 0
+    while done < evolve:
+        k = min(5000, evolve - done)
+        ob = sim.step(k)
+        done += k
+        print(f"  evolved {done}/{evolve}: bond_num {int(ob[-1]['bond_num'])} ({time.time() - t:.0f}s)",
+              file=sys.stderr, flush=True)
+    st = sim.get_state()
+    assert st.step == evolve
+    obs = sim.step(window)
+    h = engine.state_hash(p, sim.get_state())
+    sim.close()
+    o = O.Oracle(p, nbmode=O.NB_CELLS)
+    o.set_state(st)
+    obs_o, _ = o.step(window, want_hashes=False)
+    for s in range(window):
+        assert obs[s] == obs_o[s], f"step {evolve + s + 1}: gpu {obs[s]} oracle {obs_o[s]}"
+    assert h == o.hash()
+    return o.stats(), obs
+
+
+@pytest.mark.timeout(600)
+def test_c3_steady_state_window():
+    # C3: 1e6 particles, reference physics, 20 000 steps evolved, 12-step window
+    p = workloads.params("C3", seed=1)
+    ev, obs = _evolved_window(p, 20000, 12)
+    print("  C3 window events", ev, file=sys.stderr)
+    assert obs[-1]["bond_num"] > 1000
+    for k in ("complex", "laydown", "reject", "rl", "snap_bond"):
+        assert ev[k] > 0, k
+
+
+@pytest.mark.timeout(600)
+def test_c3_reaction_heavy_steady_state_window():
+    # C3's box and population with the dense scenario's reaction rates (cis
+    # association x200, dissociations 1e7-1e8 x the reference): every reaction
+    # and dissociation type inside the window, multi-ligand complexes
+    p = workloads.params("C3", seed=2, **RATES)
+    ev, obs = _evolved_window(p, 20000, 12)
+    print("  C3-heavy window events", ev, file=sys.stderr)
+    assert obs[-1]["bond_num_mono_cis"] > 0 and obs[-1]["bond_num_cis"] > 0
+    for k in ("complex", "multi", "reject", "rl", "mono", "cis", "rld", "md", "cd", "snap_bond", "snap_cis"):
+        assert ev[k] > 0, k

@@ -79,3 +79,29 @@ def test_portable_libm_exact_points():
     assert engine.math(3, np.array([1.0]))[0] == 0.0
     r = engine.math(6, np.array([2.5, -2.5, 0.49999999999999994, -0.5, 1e17]))
     assert list(r) == [3.0, -3.0, 0.0, -1.0, 1e17]
+
+
+BRUTE_CASES = [(4000, 1500), (20000, 7000)]
+
+
+@pytest.mark.parametrize("n_a,n_b", BRUTE_CASES)
+def test_cells_equal_brute_fixture_at_scale(n_a, n_b):
+    # the cell-list oracle (the only CPU checker of the GPU at C2/C3/C5) equals
+    # brute force — every pair tested, like main.cpp — step for step at
+    # thousands of proteins; brute force is O(N^2), so its per-step hashes were
+    # stored once (tests/golden/make_brute_cells.py)
+    import os
+    from _kmc import GOLDEN
+    path = os.path.join(GOLDEN, f"brute_{n_a}_{n_b}.npz")
+    if not os.path.exists(path):
+        pytest.skip("fixture not generated")
+    g = np.load(path, allow_pickle=False)
+    L = float(g["box"])
+    p = params(n_a=n_a, n_b=n_b, seed=int(g["seed"]), box_x=L, box_y=L, box_z=250.0,
+               **{k: v for k, v in DENSE.items() if not k.startswith("box")})
+    o = O.Oracle(p, nbmode=O.NB_CELLS)
+    o.set_state(engine.host_init_random(p))
+    obs, hashes = o.step(int(g["steps"]))
+    assert np.array_equal(hashes, g["hashes"])
+    assert np.array_equal(obs, g["obs"])
+    assert obs[-1]["bond_num"] > 0

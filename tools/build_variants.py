@@ -1,6 +1,8 @@
 """Timing builds for A/B runs on the GPU box (diagnostic only, never the
-product): lib/variants/libkmc_<tag>.so built with extra -D flags, selected at
-run time with KMC_LIB_PATH.
+product): ab_variants/libkmc_<tag>.so (repo root, git-ignored) built with extra
+-D flags, selected at run time with KMC_DIAG=1 KMC_LIB_PATH=...  The directory
+travels to the GPU box only while it exists: delete it after an A/B session
+(the default push carries the in-tree build alone).
   python tools/build_variants.py tag=-DFLAG[,-DFLAG2] ...
 """
 import os
@@ -11,7 +13,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
                                 "kmc-with-a-diffusion-reaction-algorithm_amd"))
 import build as B  # noqa: E402
 
-out = os.path.join(B.LIB_DIR, "variants")
+out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ab_variants")
 os.makedirs(out, exist_ok=True)
 procs = []
 for spec in sys.argv[1:]:

@@ -13,7 +13,7 @@ cd "$root"
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "$kexpr" > "$out/tests.log" 2>&1
 timeout -k 10 200 python bench.py --no-cpu-baseline > "$out/bench_base.json" 2> "$out/bench_base.err"
 for v in "$@"; do
-  KMC_LIB_PATH=$root/kmc-with-a-diffusion-reaction-algorithm_amd/lib/variants/libkmc_$v.so \
+  KMC_DIAG=1 KMC_LIB_PATH=$root/ab_variants/libkmc_$v.so \
     timeout -k 10 200 python bench.py --no-cpu-baseline > "$out/bench_$v.json" 2> "$out/bench_$v.err"
 done
 timeout -k 10 200 python bench.py --no-cpu-baseline > "$out/bench_base2.json" 2> "$out/bench_base2.err"
