@@ -103,6 +103,10 @@ def parse(argv):
     ap.add_argument("--cpu-baseline-steps", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fresh-window", action="store_true")
+    ap.add_argument("--save-state", default="", help="write the exact state after the evolution (KMCSTAT1)")
+    ap.add_argument("--load-state", default="",
+                    help="start from an exact state file instead of placement + fresh window + evolution "
+                         "(profiling the steady state without tracing the evolution)")
     ap.add_argument("--profile", action="store_true", help="print the per-kernel breakdown to stderr")
     ap.add_argument("--launcher-check", action="store_true",
                     help="ranks rendezvous over gloo and report who they are; no GPU work (launcher test)")
@@ -215,7 +219,12 @@ def run_rank(args, rank: int, world: int, local: int):
     n = p.n_a + p.n_b
     sim = engine.Simulation(p, device=local)
     t0 = time.perf_counter()
-    sim.init_random()
+    if args.load_state:
+        sim.load_state(args.load_state)
+        args.no_fresh_window = True
+        evolve = 0
+    else:
+        sim.init_random()
     t_init = time.perf_counter() - t0
 
     def barrier():
@@ -257,6 +266,8 @@ def run_rank(args, rank: int, world: int, local: int):
             print(f"bench: evolved {done}/{evolve} steps, bond_num {int(ob[-1]['bond_num'])}", file=sys.stderr,
                   flush=True)
     t_evolve = time.perf_counter() - t0
+    if args.save_state:
+        sim.save_state(args.save_state)
 
     # warm-up with every kernel bracketed: find the dominant kernel
     sim.set_timing(engine.kernel_names())
@@ -311,6 +322,7 @@ def run_rank(args, rank: int, world: int, local: int):
                 "box_A": [p.box_x, p.box_y, p.box_z],
                 "parallelism": f"replicas x{world} (independent trajectories, RCCL all-reduce of observables)",
                 "evolve_steps": evolve,
+                "start_state": args.load_state or "keyed placement",
                 "timed_from_step": sim.current_step - args.steps,
                 "ms_per_step_fresh": fresh_ms,
                 "per_rank_ms_per_step": [x / args.steps * 1e3 for x in per_rank],

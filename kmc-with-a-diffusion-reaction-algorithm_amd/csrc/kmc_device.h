@@ -30,7 +30,6 @@ struct KParams {
   kmcr::Key key;
   int tcap;  // LDS tile record capacity (<= TCAP; lowered only to test the global path)
   int tile;  // cells per tile side of the LDS scans (<= TILE_MAX)
-  int cx_blocks;  // workgroups of k_complex (one wave per complex)
   int dbg_stage;  // debug timing only: stop the tile scans after stage 1 (load) / 2 (items); 0 = off
 };
 
@@ -44,7 +43,9 @@ struct Ctl {
   uint32_t n_overflow;    // ligands whose BFS overflowed the register queue
   uint32_t cx_cursor;     // members[] allocation cursor
   uint32_t n_pend;        // units still pending after a round (pass C)
-  uint32_t n_cx;          // complexes registered by the BFS this step
+  uint32_t n_cx;          // complexes registered by the BFS this step (cx_list)
+  uint32_t n_heavy;       // entries of cx_heavy this step
+  uint32_t pad1;
   uint32_t last[8];       // previous step's work counts (diagnostics): cand conf plist rej pairs rl cisc overflow
   uint32_t n_rl;          // R–L accepting edges
   uint32_t n_cisc;        // cis candidates
@@ -53,7 +54,7 @@ struct Ctl {
   int32_t maxc;                                 // protein_num_in_Max_Complex
   int32_t pad2;
   uint64_t vtag;          // BFS tag counter for the overflow path
-  uint64_t stamps[16];    // diagnostic build (-DKMC_STAMPS) only: tile-scan phase cycles
+  uint64_t stamps[24];    // diagnostic build (-DKMC_STAMPS) only: phase cycles (tile scans, complexes)
 };
 
 enum : uint32_t {

@@ -19,12 +19,12 @@ using namespace kmcd;
 
 // kernel ids for per-kernel HIP-event timing (kmc_set_timing / kmc_kernel_times)
 enum KId {
-  KI_CLASSIFY, KI_BFS, KI_BFS_OVF, KI_PROPOSE, KI_COMPLEX, KI_REC_COUNT, KI_SCAN, KI_REC_SCATTER,
+  KI_CLASSIFY, KI_BFS, KI_PROPOSE, KI_PROPOSE_FREE, KI_COMPLEX, KI_CX_HEAVY, KI_SCAN, KI_REC_SCATTER,
   KI_COL_SCAN, KI_COL_EXACT, KI_COL_ROUNDS, KI_COMMIT, KI_RXN_SCAN, KI_RXN_EXACT, KI_MATCH, KI_DISS_OBSERVE,
   KI_RESORT, KI_N
 };
 static const char* const KNAMES[KI_N] = {
-    "k_classify", "k_bfs", "k_bfs_overflow", "k_propose", "k_complex", "k_rec_count", "k_scan",
+    "k_classify", "k_bfs", "k_propose", "k_propose_free", "k_complex", "k_complex_heavy", "k_scan",
     "k_rec_scatter", "k_col_scan", "k_col_exact", "k_col_rounds", "k_commit", "k_rxn_scan", "k_rxn_exact",
     "k_match", "k_diss_observe", "slot_resort"};
 #define TRING 64  // steps of event pairs kept in flight
@@ -35,6 +35,14 @@ struct kmc_sim {
   Dev d;
   int device = 0;
   hipStream_t stream = nullptr;
+  // complexes: 1 = the complex kernels then k_propose_free on the stream,
+  // 2 = the complex kernels on a side stream beside k_propose_free,
+  // 3 = k_propose_free then the complex kernels
+  int cx_mode = 1;
+  int cx_grid = 0;
+  size_t free_lds = 0;  // debug (KMC_FREE_LDS): dynamic LDS reserved by k_propose_free, to cap its occupancy
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int64_t step_done = 0;
   std::string err;
   int ncell = 0;
@@ -56,7 +64,8 @@ struct kmc_sim {
   // slot order (kmc_kernels.hip §slot order): scratch of the re-sort
   int64_t resort_every = 100, since_resort = 0;
   int key_bits = 1;
-  uint32_t *skeys = nullptr, *skeys2 = nullptr;
+  uint64_t *skeys = nullptr, *skeys2 = nullptr;  // (cell << 32) | grouping key
+  bool group_sort = true;  // members of one unit in consecutive slots (KMC_GROUP_SORT=0: cell only)
   int32_t *svals = nullptr, *svals2 = nullptr, *perm = nullptr, *newslot = nullptr;
   int32_t *a_tmp = nullptr, *b_tmp = nullptr, *id_tmp = nullptr;
   void* sort_tmp = nullptr;
@@ -286,6 +295,7 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   rc |= dalloc(s, &d.pend, N);
   rc |= dalloc(s, &d.overflow, NB);
   rc |= dalloc(s, &d.cx_list, NB);
+  rc |= dalloc(s, &d.cx_heavy, NB);
   rc |= dalloc(s, &d.cell_cnt, s->ncell + 1);
   rc |= dalloc(s, &d.cell_cnt_alt, s->ncell + 1);
   d.ncnt = s->ncell + 1;
@@ -328,7 +338,38 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
     if (te && *te) t = std::max(2, std::min(TILE_MAX, atoi(te)));
     K.tile = t;
     // k_complex waves: up to one per 4 ligands, at most 4096
-    K.cx_blocks = NB > 0 ? std::min(1024, (NB + 15) / 16) : 0;
+    const char* cm = getenv("KMC_CX_MODE");
+    if (cm && *cm) s->cx_mode = std::max(1, std::min(4, atoi(cm)));
+    // k_complex: enough 4-wave workgroups to fill every CU (dynamic dispatch:
+    // surplus workgroups find the list empty and exit)
+    s->cx_grid = NB > 0 ? std::min(2048, (NB + 15) / 16) : 0;
+    const char* fl = getenv("KMC_FREE_LDS");
+    if (fl && *fl) s->free_lds = (size_t)std::max(0, std::min(160 * 1024, atoi(fl)));
+    const char* cg = getenv("KMC_CX_GRID");
+    if (cg && *cg) s->cx_grid = std::max(1, atoi(cg));
+    if (s->cx_mode == 2 || s->cx_mode == 4) {
+      // KMC_SIDE_CUS=n: the side stream's kernels on n CUs spread over the
+      // XCDs (CU mask), the rest of the chip left to the main stream's stream
+      const char* sc = getenv("KMC_SIDE_CUS");
+      int ncu = sc && *sc ? atoi(sc) : 0;
+      hipError_t e = hipSuccess;
+      if (ncu > 0 && ncu < prop.multiProcessorCount) {
+        const int tot = prop.multiProcessorCount;
+        std::vector<uint32_t> mask((tot + 31) / 32, 0u);
+        for (int i = 0; i < ncu; ++i) {
+          const int cu = (int)((int64_t)i * tot / ncu);
+          mask[cu / 32] |= 1u << (cu % 32);
+        }
+        e = hipExtStreamCreateWithCUMask(&s->side, (uint32_t)mask.size(), mask.data());
+      } else {
+        e = hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking);
+      }
+      if (e != hipSuccess || hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming) != hipSuccess) {
+        kmc_destroy(s);
+        return KMC_ERR_HIP;
+      }
+    }
     const char* ds = getenv("KMC_DEBUG_SCAN_STAGE");
     K.dbg_stage = ds && *ds ? atoi(ds) : 0;
   }
@@ -341,8 +382,10 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
     if (re && *re) s->resort_every = atoll(re);
     size_t tb = 0;
     int nmax = std::max(NA, NB);
+    const char* gs = getenv("KMC_GROUP_SORT");
+    if (gs && *gs) s->group_sort = *gs != '0';
     if (hipcub::DeviceRadixSort::SortPairs(nullptr, tb, s->skeys, s->skeys2, s->svals, s->svals2, nmax, 0,
-                                           s->key_bits, s->stream) != hipSuccess) {
+                                           32 + s->key_bits, s->stream) != hipSuccess) {
       kmc_destroy(s);
       return KMC_ERR_HIP;
     }
@@ -375,6 +418,10 @@ int kmc_destroy(kmc_sim* s) {
   if (s->ctl_host) (void)hipHostFree(s->ctl_host);
   for (auto& e : s->tev)
     if (e) (void)hipEventDestroy(e);
+  if (s->side) (void)hipStreamSynchronize(s->side);
+  if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);
+  if (s->ev_join) (void)hipEventDestroy(s->ev_join);
+  if (s->side) (void)hipStreamDestroy(s->side);
   if (s->stream) (void)hipStreamDestroy(s->stream);
   delete s;
   return KMC_OK;
@@ -419,15 +466,16 @@ static int resort(kmc_sim* s) {
   Dev& d = s->d;
   hipStream_t st = s->stream;
   const int NA = K.NA, NB = K.NB, N = K.N, T = 256;
-  k_slot_keys<<<(N + T - 1) / T, T, 0, st>>>(K, d, s->skeys, s->svals);
+  k_slot_keys<<<(N + T - 1) / T, T, 0, st>>>(K, d, s->skeys, s->svals, s->group_sort);
+  const int b0 = s->group_sort ? 0 : 32, b1 = 32 + s->key_bits;
   size_t tb = s->sort_tmp_bytes;
   if (NA > 0)
-    HIPCHK(s, hipcub::DeviceRadixSort::SortPairs(s->sort_tmp, tb, s->skeys, s->skeys2, s->svals, s->svals2, NA, 0,
-                                                 s->key_bits, st));
+    HIPCHK(s, hipcub::DeviceRadixSort::SortPairs(s->sort_tmp, tb, s->skeys, s->skeys2, s->svals, s->svals2, NA, b0,
+                                                 b1, st));
   tb = s->sort_tmp_bytes;
   if (NB > 0)
     HIPCHK(s, hipcub::DeviceRadixSort::SortPairs(s->sort_tmp, tb, s->skeys + NA, s->skeys2 + NA, s->svals + NA,
-                                                 s->svals2 + NA, NB, 0, s->key_bits, st));
+                                                 s->svals2 + NA, NB, b0, b1, st));
   k_slot_inverse<<<(N + T - 1) / T, T, 0, st>>>(K, s->svals2, s->perm, s->newslot);
   reorder(s, s->perm, s->newslot, true);
   k_gather_ids<<<(N + T - 1) / T, T, 0, st>>>(K, d.id_of, s->id_tmp, d.slot_of, s->perm);
@@ -510,6 +558,8 @@ int kmc_set_state(kmc_sim* s, const kmc_state_view* v) {
   HIPCHK(s, hipMemcpy(d.ctl, &c, sizeof c, hipMemcpyHostToDevice));
   rc = clear_step_tags(s);
   if (rc != KMC_OK) return rc;
+  // no unit keys yet: the first slot sort groups by cell only
+  HIPCHK(s, hipMemsetAsync(d.owner, 0xff, sizeof(int32_t) * (size_t)(NA + NB), s->stream));
   // reference order = identity slots, then the spatial sort
   k_iota<<<(NA + NB + 255) / 256, 256, 0, s->stream>>>(d.id_of, d.slot_of, NA + NB);
   if (NA > 0)
@@ -667,11 +717,45 @@ static int launch_step(kmc_sim* s, bool re_sort) {
     (void)hipMemsetAsync(d.nxt.b, 0xff, sizeof(double) * 24 * (size_t)K.NB, st);
   }
   TIMED(KI_CLASSIFY, (k_classify<<<gN, T, 0, st>>>(K, d)));
+  if (s->cx_mode == 4 && K.NB > 0) {
+    // the complex chain (BFS, moves, heavy path) on the side stream beside the
+    // free units: k_propose_free reads only k_classify's unit kinds; the two
+    // sides touch disjoint proteins and count records with commutative atomics
+    Bracket b_(s, KI_PROPOSE, st);
+    HIPCHK(s, hipEventRecord(s->ev_fork, st));
+    HIPCHK(s, hipStreamWaitEvent(s->side, s->ev_fork, 0));
+    TIMED_ON(KI_BFS, s->side, (k_bfs<<<gB, T, 0, s->side>>>(K, d)));
+    TIMED_ON(KI_COMPLEX, s->side, (k_complex<<<s->cx_grid, T, 0, s->side>>>(K, d)));
+    TIMED_ON(KI_CX_HEAVY, s->side, (k_complex_heavy<<<256, T, 0, s->side>>>(K, d)));
+    HIPCHK(s, hipEventRecord(s->ev_join, s->side));
+    TIMED(KI_PROPOSE_FREE, (k_propose_free<<<gN, T, s->free_lds, st>>>(K, d)));
+    HIPCHK(s, hipStreamWaitEvent(st, s->ev_join, 0));
+  } else {
   if (K.NB > 0) {
     TIMED(KI_BFS, (k_bfs<<<gB, T, 0, st>>>(K, d)));
   }
-  // complexes (one wave each) and the free units in one launch
-  TIMED(KI_PROPOSE, (k_propose<<<K.cx_blocks + gN, T, 0, st>>>(K, d)));
+  // complexes (a wave each: rigid move, lay-down / alignment, record
+  // counts) beside the free units' HBM stream (side
+  // stream) or before it; disjoint proteins, commutative record-count atomics
+  hipStream_t cs = s->cx_mode == 2 ? s->side : st;
+  // KI_PROPOSE brackets the whole proposal phase (fork to join): every
+  // protein's R read and R_new written once, the bench's roofline unit
+  {
+    Bracket b_(s, KI_PROPOSE, st);
+    if (s->cx_mode == 3) TIMED(KI_PROPOSE_FREE, (k_propose_free<<<gN, T, s->free_lds, st>>>(K, d)));
+    if (K.NB > 0) {
+      if (s->cx_mode == 2) {
+        HIPCHK(s, hipEventRecord(s->ev_fork, st));
+        HIPCHK(s, hipStreamWaitEvent(s->side, s->ev_fork, 0));
+      }
+      TIMED_ON(KI_COMPLEX, cs, (k_complex<<<s->cx_grid, T, 0, cs>>>(K, d)));
+      TIMED_ON(KI_CX_HEAVY, cs, (k_complex_heavy<<<256, T, 0, cs>>>(K, d)));
+      if (s->cx_mode == 2) HIPCHK(s, hipEventRecord(s->ev_join, s->side));
+    }
+    if (s->cx_mode != 3) TIMED(KI_PROPOSE_FREE, (k_propose_free<<<gN, T, s->free_lds, st>>>(K, d)));
+    if (K.NB > 0 && s->cx_mode == 2) HIPCHK(s, hipStreamWaitEvent(st, s->ev_join, 0));
+  }
+  }
   TIMED(KI_SCAN, {
     // single-pass decoupled look-back scan; cell_cnt[ncell] stays 0, so
     // cell_start[ncell] is the record total
@@ -793,6 +877,10 @@ int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out) {
               (long long)s->step_done, l[0], l[1], l[2], l[3], l[4], l[5], l[6], l[7], s->grow,
               (long long)s->n_replays);
       const uint64_t* t = s->ctl_host->stamps;
+      if (t[16])
+        fprintf(stderr, "kmc stamps cx stage %llu rigid %llu checks %llu writeback %llu count %llu next %llu\n",
+                (unsigned long long)t[16], (unsigned long long)t[17], (unsigned long long)t[18],
+                (unsigned long long)t[19], (unsigned long long)t[20], (unsigned long long)t[21]);
       if (t[0] | t[8])
         fprintf(stderr, "kmc stamps col %llu %llu %llu %llu %llu %llu %llu %llu rxn %llu %llu %llu %llu %llu %llu %llu %llu\n",
                 (unsigned long long)t[0], (unsigned long long)t[1], (unsigned long long)t[2], (unsigned long long)t[3],

@@ -56,7 +56,9 @@ struct Dev {
   int32_t* members;  // [N]
   uint32_t* pend;    // [N] round tag: unit still waiting (resolution pass C)
   int32_t* overflow; // [NB]
-  int32_t* cx_list;  // [NB] ligand (B index) of every complex root this step
+  int4* cx_list;     // [NB] descriptors of this step's complexes of <= CXL members (k_complex)
+  int4* cx_heavy;    // [NB] descriptors for k_complex_heavy: larger complexes, and those k_complex
+                     //      moved but whose lay-down / alignment changes beads
   int32_t* cell_cnt;    // [ncell+1] this step's record counts (counted by the proposals, read by the scan)
   int32_t* cell_cnt_alt;  // [ncell+1] the next step's counts: zeroed by k_diss_observe, swapped after the step
   int ncnt;             // ncell+1
@@ -162,31 +164,13 @@ __global__ void k_classify(KParams P, Dev d) {
 // Complex of ligand root b: BFS over the bond graph exactly as
 // main.cpp:525-561 (receptor neighbours res_nei[2], [3]; ligand neighbours
 // res_nei[2], [3], [4]; a node is enqueued when first seen).  The root is the
-// lowest-indexed ligand of its component; a BFS that meets a lower ligand
-// stops (that ligand owns the component).
-#define BFS_QCAP 96
-__device__ __forceinline__ int nbrs(const KParams& P, const Dev& d, int x, int* y) {
-  const int NA = P.NA, NB = P.NB;
-  int n = 0;
-  if (x < NA) {
-    int v = A_NEI2(d, x);
-    if (v > 0) y[n++] = v - 1;
-    v = A_NEI3(d, x);
-    if (v > 0) y[n++] = v - 1;
-  } else {
-    int b = x - NA;
-    for (int j = 2; j <= 4; ++j) {
-      int v = B_NEI(d, b, j);
-      if (v > 0) y[n++] = v - 1;
-    }
-  }
-  return n;
-}
+// lowest-indexed ligand of its component; the BFS of any other ligand of the
+// component finds a lower one among its members and registers nothing.
+#define BFS_QCAP 32
+#define BFS_BATCH 4
+#define CXL 16  // members of a complex staged in LDS by k_complex (see §complexes)
 
-// listed: append the root to cx_list (k_complex's work list); the overflow
-// path moves its complexes itself
-// the same neighbours in three fixed slots (-1 = none), for code that must
-// not index a local array dynamically (k_complex: no scratch)
+// the neighbours in three fixed slots (-1 = none), in BFS order
 __device__ __forceinline__ void nbrs3(const KParams& P, const Dev& d, int x, int* y) {
   const int NA = P.NA, NB = P.NB;
   if (x < NA) {
@@ -203,56 +187,146 @@ __device__ __forceinline__ void nbrs3(const KParams& P, const Dev& d, int x, int
   }
 }
 
+// slot for each calling lane (call from the lanes that emit)
+__device__ __forceinline__ uint32_t wave_slot(uint32_t* ctr) {
+  const uint64_t mask = __ballot(1);
+  const int lane = __lane_id();
+  const int leader = __ffsll((unsigned long long)mask) - 1;
+  const uint32_t rank = __popcll(mask & ((1ull << lane) - 1ull));
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(ctr, (uint32_t)__popcll(mask));
+  base = __shfl(base, leader, 64);
+  return base + rank;
+}
+
+// members[] range of qn entries for each calling lane: one atomic per wave
+// (the lanes that reach it together), not per complex — a single counter
+// word serialises its atomics (MI355X_MICROARCH.md)
+__device__ __forceinline__ uint32_t wave_alloc(uint32_t* ctr, uint32_t qn) {
+  const uint64_t mask = __ballot(1);
+  const int lane = __lane_id(), leader = __ffsll((unsigned long long)mask) - 1;
+  uint32_t pre = 0, tot = 0;
+  for (uint64_t m = mask; m; m &= m - 1) {
+    const int l = __ffsll((unsigned long long)m) - 1;
+    const uint32_t v = (uint32_t)__shfl((int)qn, l, 64);
+    pre += l < lane ? v : 0u;
+    tot += v;
+  }
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(ctr, tot);
+  return (uint32_t)__shfl((int)base, leader, 64) + pre;
+}
+
+// Complex descriptor (cx_list / cx_heavy): x = root ligand lb | CXD_MOVED
+// (rigid move already done by k_complex), y = members[] offset, z = size |
+// ligands << 16, w = the root's reference index (its random-stream key).
+#define CXD_MOVED (1 << 30)
+#define CXD_LB 0x3fffffff
+
+// Register the component in queue q (q[t * STRIDE], t < qn, BFS order) rooted
+// at ligand slot p: member row, owner keys, descriptor — on cx_list for a
+// complex of at most CXL members (k_complex stages it in LDS), else on the
+// heavy list (global-memory path).
+template <int STRIDE = 1>
 __device__ __forceinline__ void register_complex(const KParams& P, const Dev& d, int p, const int* q, int qn, bool listed) {
-  uint32_t off = atomicAdd(&d.ctl->cx_cursor, (uint32_t)qn);
-  if (off + qn > (uint32_t)P.N) {
+  const int NA = P.NA, NB = P.NB;
+  uint32_t off = wave_alloc(&d.ctl->cx_cursor, (uint32_t)qn);
+  if (off + qn > (uint32_t)P.N) {  // inconsistent bond graph: the step is undone (kmc_step)
     atomicOr(&d.ctl->err, ERR_MEMBERS);
-    return;
+    qn = 0;
+    off = 0;
   }
   int nb = 0;
+  const int rootid = d.id_of[p];
+#pragma unroll 4
   for (int t = 0; t < qn; ++t) {
-    int m = q[t];
+    int m = q[t * STRIDE];
     d.members[off + t] = m;
-    d.owner[m] = d.id_of[p];
-    nb += m >= P.NA;
+    d.owner[m] = rootid;
+    nb += m >= NA;
   }
-  int b = p - P.NA;
+  const bool staged = listed && qn <= CXL;
+  int b = p - NA;
   d.cx_off[b] = (int)off;
   d.cx_size[b] = qn;
   d.cx_nb[b] = nb;
   d.ukind[p] = U_COMPLEX;
-  if (listed) d.cx_list[atomicAdd(&d.ctl->n_cx, 1u)] = b;
+  if (listed) {
+    const int4 desc = make_int4(b, (int)off, qn | nb << 16, rootid);
+    if (staged) d.cx_list[wave_slot(&d.ctl->n_cx)] = desc;
+    else d.cx_heavy[wave_slot(&d.ctl->n_heavy)] = desc;
+  }
 }
 
-__global__ void k_bfs(KParams P, Dev d) {
+// One thread per bonded ligand; the queue lives in LDS, one column per thread
+// (consecutive lanes, consecutive banks): a dynamically indexed private
+// array would go to scratch (400 B/lane).  The lower-ligand test is made once
+// over the finished queue (independent loads), so each BFS node costs one
+// round of link loads.  Components larger than BFS_QCAP go to the overflow
+// path.
+__global__ void __launch_bounds__(256) k_bfs(KParams P, Dev d) {
+  __shared__ int qs[BFS_QCAP * 256];
   const int NA = P.NA, NB = P.NB;
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= NB) return;
   if (B_NEI(d, b, 2) == 0 && B_NEI(d, b, 3) == 0 && B_NEI(d, b, 4) == 0) return;
+  int* q = qs + threadIdx.x;  // q[t * 256]
   int p = NA + b;
   const int pid = d.id_of[p];
-  int q[BFS_QCAP];
-  int qn = 0, head = 0;
-  q[qn++] = p;
-  while (head < qn) {
-    int x = q[head++];
-    int y[3];
-    int ny = nbrs(P, d, x, y);
-    for (int e = 0; e < ny; ++e) {
-      int v = y[e];
-      if (v >= NA && d.id_of[v] < pid) return;  // a lower ligand roots this component
-      bool seen = false;
-      for (int t = 0; t < qn; ++t) seen |= q[t] == v;
-      if (seen) continue;
-      if (qn == BFS_QCAP) {
-        uint32_t s = atomicAdd(&d.ctl->n_overflow, 1u);
-        d.overflow[s] = b;
-        return;
+  auto lower = [&](int qn) {  // a lower ligand among the first qn members roots the component
+    bool lw = false;
+    for (int t0 = 1; t0 < qn; t0 += 8) {  // eight independent loads in flight
+      int id[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int t = t0 + i, v = t < qn ? q[t * 256] : 0;
+        id[i] = v >= NA ? d.id_of[v] : pid;
       }
-      q[qn++] = v;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) lw |= id[i] < pid;
     }
+    return lw;
+  };
+  int qn = 1, head = 0;
+  q[0] = p;
+  uint64_t bloom = 1ull << (((uint32_t)p * 0x9E3779B1u) >> 26);
+  // nodes are expanded in queue order; the links of the next (up to) BFS_BATCH
+  // queued nodes are loaded together first (one round of loads per batch
+  // instead of per node)
+  while (head < qn) {
+    const int nb = min(BFS_BATCH, qn - head);
+    int y[BFS_BATCH][3];
+#pragma unroll
+    for (int i = 0; i < BFS_BATCH; ++i)
+      if (i < nb) nbrs3(P, d, q[(head + i) * 256], y[i]);
+#pragma unroll
+    for (int i = 0; i < BFS_BATCH; ++i) {
+      if (i >= nb) break;
+#pragma unroll
+      for (int e = 0; e < 3; ++e) {
+        int v = y[i][e];
+        if (v < 0) continue;
+        // 64-bit filter of the queued slots: only a possible hit scans the queue
+        const uint64_t bit = 1ull << (((uint32_t)v * 0x9E3779B1u) >> 26);
+        if (bloom & bit) {
+          bool seen = false;
+          for (int t = 0; t < qn; ++t) seen |= q[t * 256] == v;
+          if (seen) continue;
+        }
+        bloom |= bit;
+        if (qn == BFS_QCAP) {
+          if (lower(qn) || (v >= NA && d.id_of[v] < pid)) return;
+          uint32_t s = atomicAdd(&d.ctl->n_overflow, 1u);
+          d.overflow[s] = b;
+          return;
+        }
+        q[(qn++) * 256] = v;
+      }
+    }
+    head += nb;
   }
-  register_complex(P, d, p, q, qn, true);
+  if (lower(qn)) return;
+  register_complex<256>(P, d, p, q, qn, true);
 }
 
 // Component of overflow entry o (larger than BFS_QCAP): one thread, global
@@ -438,7 +512,8 @@ __device__ void propose_free_a(const KParams& P, const Dev& d, int i, uint32_t s
 }
 
 // snap receptor a2 onto a1's cis site (x,y of all 16 beads), main.cpp:786-798
-__device__ __forceinline__ void snap_cis(const KParams& P, const Beads& N, int a2, int a1, double cis_cut) {
+template <class S>
+__device__ __forceinline__ void snap_cis(const KParams& P, const S& N, int a2, int a1, double cis_cut) {
   const double RA = P.ra;
   double x33 = N.A(a1, 3, 3, 0), x31 = N.A(a1, 3, 1, 0);
   double y33 = N.A(a1, 3, 3, 1), y31 = N.A(a1, 3, 1, 1);
@@ -462,7 +537,8 @@ __device__ __forceinline__ void snap_cis(const KParams& P, const Beads& N, int a
 
 // snap receptor a onto ligand site (lb = ligand 0-based in B arrays, j),
 // main.cpp:1216-1228
-__device__ __forceinline__ void snap_bond(const KParams& P, const Beads& N, int a, int lb, int j, double bond_cut) {
+template <class S>
+__device__ __forceinline__ void snap_bond(const KParams& P, const S& N, int a, int lb, int j, double bond_cut) {
   const double RA = P.ra, RB = P.rb;
   double x2 = N.B(lb, j, 2, 0), x1 = N.B(lb, j, 1, 0);
   double y2 = N.B(lb, j, 2, 1), y1 = N.B(lb, j, 1, 1);
@@ -484,16 +560,19 @@ __device__ __forceinline__ void snap_bond(const KParams& P, const Beads& N, int 
   }
 }
 
-__device__ __forceinline__ double dxyA(const Beads& N, int p, int j, int k, int q, int jj, int kk) {
+template <class S>
+__device__ __forceinline__ double dxyA(const S& N, int p, int j, int k, int q, int jj, int kk) {
   double dx = N.A(p, j, k, 0) - N.A(q, jj, kk, 0), dy = N.A(p, j, k, 1) - N.A(q, jj, kk, 1);
   return kmcm::sqrt_(dx * dx + dy * dy);
 }
 // ligand lb bead (j,k) vs receptor a bead (jj,kk)
-__device__ __forceinline__ double dxyBA(const Beads& N, int lb, int j, int k, int a, int jj, int kk) {
+template <class S>
+__device__ __forceinline__ double dxyBA(const S& N, int lb, int j, int k, int a, int jj, int kk) {
   double dx = N.B(lb, j, k, 0) - N.A(a, jj, kk, 0), dy = N.B(lb, j, k, 1) - N.A(a, jj, kk, 1);
   return kmcm::sqrt_(dx * dx + dy * dy);
 }
-__device__ __forceinline__ bool cis_misaligned(const KParams& P, const Beads& N, int a1, int a2) {
+template <class S>
+__device__ __forceinline__ bool cis_misaligned(const KParams& P, const S& N, int a1, int a2) {
   double dd2 = dxyA(N, a1, 3, 3, a2, 3, 3);
   double dd1 = dxyA(N, a1, 3, 1, a2, 3, 1);
   return !AreSame(dd1, P.cis_cut / 2 + P.ra + P.ra) || !AreSame(dd2, P.cis_cut / 2);
@@ -501,7 +580,8 @@ __device__ __forceinline__ bool cis_misaligned(const KParams& P, const Beads& N,
 __device__ __forceinline__ bool bond_mis_d(const KParams& P, double dd1, double dd2) {
   return !AreSame(dd1, P.bond_cut / 2 + P.ra + P.rb) || !AreSame(dd2, P.bond_cut / 2);
 }
-__device__ __forceinline__ bool bond_misaligned(const KParams& P, const Beads& N, int lb, int j, int a1) {
+template <class S>
+__device__ __forceinline__ bool bond_misaligned(const KParams& P, const S& N, int lb, int j, int a1) {
   double dd2 = dxyBA(N, lb, j, 2, a1, 3, 2);
   double dd1 = dxyBA(N, lb, j, 1, a1, 3, 1);
   return bond_mis_d(P, dd1, dd2);
@@ -653,27 +733,98 @@ __device__ __forceinline__ void propose_one(const KParams& P, const Dev& d, int 
   }
 }
 
+// ---------------------------------------------------------------- stamps
+// Diagnostic build only (-DKMC_STAMPS): thread 0 of each workgroup adds the
+// cycles since its previous stamp to ctl->stamps[base + i] (phase shares of
+// the tile scans; kmc_step prints them with KMC_DEBUG_COUNTS=1).  In the
+// real build a stamp compiles to nothing.
+struct Stamper {
+#ifdef KMC_STAMPS
+  uint64_t t;
+  int base;
+  __device__ static uint64_t now() {
+    uint64_t v;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");
+    return v;
+  }
+  __device__ explicit Stamper(int b) : t(now()), base(b) {}
+  __device__ void operator()(const Dev& d, int i) {
+    if (threadIdx.x == 0) {
+      const uint64_t v = now();
+      atomicAdd((unsigned long long*)&d.ctl->stamps[base + i], (unsigned long long)(v - t));
+      t = v;
+    }
+  }
+#else
+  __device__ explicit Stamper(int) {}
+  __device__ void operator()(const Dev&, int) {}
+#endif
+};
+
 // ---------------------------------------------------------------- complexes
 // Ligand-rooted complex of size > 1: rigid move (main.cpp:974-1131), lay-down
 // of a single ligand (1138-1193), receptor / cis re-alignment (1196-1274),
-// multi-ligand alignment (1284-1732).  One thread per complex runs the
-// sequential code on R (d.cur) and R_new (d.nxt).
-struct Cx {
-  const KParams& P;
-  const Dev& d;
+// multi-ligand alignment (1284-1732) — one wave per complex (k_complex).
+//
+// A complex of up to CXL members is staged in LDS: the wave loads the member
+// slots and links, moves the beads (lanes over (member, bead)) into LDS, lane
+// 0 runs the sequential, data-dependent lay-down / alignment code against LDS
+// (a dependent chain of LDS accesses instead of HBM round trips — the step's
+// critical path at the bond-rich steady state), then the lanes write R_new
+// back and count the members' records.  Members are addressed by their
+// position t in the BFS row, encoded like protein numbers so that the
+// reference's kind tests carry over unchanged: receptor t -> t, ligand t ->
+// NA + t.  Larger complexes (rare) run the same code on global memory.
+struct CxLds {
+  double bead[CXL][48];  // R_new of member t: receptor bead (j,k) at ((j-1)*4+(k-1))*3+c, ligand ((j-1)*2+(k-1))*3+c
+  int lk[CXL][4];        // links (encoded): receptor {nei4 (site), nei2, nei3, -}, ligand {-, nei2, nei3, nei4}
+  int slot[CXL];         // slot of member t
+  int res[CXL];          // member row (encoded), shuffled in place like results[c][.]
+  uint8_t mv[CXL];       // moved flags of this step (main.cpp:122)
+};
+struct LdsBeads {
+  CxLds* L;
+  __device__ double& A(int t, int j, int k, int c) const { return L->bead[t][((j - 1) * 4 + (k - 1)) * 3 + c]; }
+  __device__ double& B(int t, int j, int k, int c) const { return L->bead[t][((j - 1) * 2 + (k - 1)) * 3 + c]; }
+};
+// links and moved flags of a staged complex
+struct LdsLinks {
+  CxLds* L;
+  int NA;
+  __device__ int a2(int a) const { return L->lk[a][1]; }
+  __device__ int a3(int a) const { return L->lk[a][2]; }
+  __device__ int a4(int a) const { return L->lk[a][0]; }
+  __device__ int b(int lb, int j) const { return L->lk[lb][j - 1]; }
+  __device__ bool moved(int m) const { return L->mv[m < NA ? m : m - NA] != 0; }
+  __device__ void set_moved(int m) const { L->mv[m < NA ? m : m - NA] = 1; }
+};
+// the global state rows (slots)
+struct GlbLinks {
+  const Dev* d;
+  int NA, NB;
   uint32_t step;
-  int root;  // slot of the root ligand
-  uint32_t rootid;  // its reference index (random stream key)
-  int* res;  // member row (BFS order, shuffled in place like results[c][.])
+  __device__ int a2(int a) const { return d->a_int[2 * (size_t)NA + a]; }
+  __device__ int a3(int a) const { return d->a_int[4 * (size_t)NA + a]; }
+  __device__ int a4(int a) const { return d->a_int[3 * (size_t)NA + a]; }
+  __device__ int b(int lb, int j) const { return d->b_int[(size_t)(4 + j - 1) * NB + lb]; }
+  __device__ bool moved(int m) const { return d->moved[m] == step + 1; }
+  __device__ void set_moved(int m) const { d->moved[m] = step + 1; }
+};
+
+template <class S, class L>
+struct CxT {
+  const KParams& P;
+  uint32_t step;
+  uint32_t rootid;  // the root ligand's reference index (random stream key)
+  int* res;         // member row (BFS order, shuffled in place like results[c][.])
   int size;
-  __device__ bool isA(int m) const { return m < P.NA; }
-  __device__ double& N(int m, int j, int k, int c) const { return d.nxt.P(m, j, k, c); }
-  __device__ double& R(int m, int j, int k, int c) const { return d.cur.P(m, j, k, c); }
-  __device__ int nk(int m) const { return m < P.NA ? 4 : 2; }
-  __device__ int neiA2(int a) const { const int NA = P.NA; return A_NEI2(d, a); }
-  __device__ int neiA3(int a) const { const int NA = P.NA; return A_NEI3(d, a); }
-  __device__ int neiA4(int a) const { const int NA = P.NA; return A_NEI4(d, a); }
-  __device__ int neiB(int lb, int j) const { const int NB = P.NB; return B_NEI(d, lb, j); }
+  S N;              // R_new
+  L lk;
+  uint32_t* err;
+  __device__ int neiA2(int a) const { return lk.a2(a); }
+  __device__ int neiA3(int a) const { return lk.a3(a); }
+  __device__ int neiA4(int a) const { return lk.a4(a); }
+  __device__ int neiB(int lb, int j) const { return lk.b(lb, j); }
   // res_nei_new[x][j] with reference semantics for the alignment code, where
   // x may be a receptor or a ligand (reference index, 0 = the empty row 0)
   __device__ int rnei(int x_ref, int j) const {
@@ -682,8 +833,8 @@ struct Cx {
     if (x < P.NA) return j == 2 ? neiA2(x) : j == 3 ? neiA3(x) : j == 4 ? neiA4(x) : 0;
     return j >= 1 && j <= 4 ? neiB(x - P.NA, j) : 0;
   }
-  __device__ bool is_moved(int m) const { return d.moved[m] == step + 1; }
-  __device__ void set_moved(int m) const { d.moved[m] = step + 1; }
+  __device__ bool is_moved(int m) const { return lk.moved(m); }
+  __device__ void set_moved(int m) const { lk.set_moved(m); }
   __device__ uint32_t shuf_rand(uint32_t call, uint32_t pos) const {
     return kmcr::rand31(P.key, kmcr::DOM_SHUF, rootid, call, step, pos);
   }
@@ -713,9 +864,10 @@ __device__ __forceinline__ void ligand_template(double rb, double tx[5][3], doub
 }
 
 // body of lable4, main.cpp:1441-1583; returns protein_B_index (0-based) after it
-__device__ __forceinline__ int step2_body(const Cx& X, int B, int j, int a1) {
+template <class CX>
+__device__ __forceinline__ int step2_body(const CX& X, int B, int j, int a1) {
   const KParams& P = X.P;
-  const Beads& N = X.d.nxt;
+  const auto& N = X.N;
   const int NA = P.NA;
   X.set_moved(B);
   int lb = B - NA;
@@ -769,9 +921,10 @@ __device__ __forceinline__ int step2_body(const Cx& X, int B, int j, int a1) {
   return Bref - 1;
 }
 
-__device__ __forceinline__ void multi_ligand_align(const Cx& X) {
+template <class CX>
+__device__ __forceinline__ void multi_ligand_align(const CX& X) {
   const KParams& P = X.P;
-  const Beads& N = X.d.nxt;
+  const auto& N = X.N;
   const int NA = P.NA;
   const int csize = X.size;
   int* res = X.res;
@@ -812,7 +965,7 @@ __device__ __forceinline__ void multi_ligand_align(const Cx& X) {
   double jd1 = 0, jd2 = 0;
   for (int guard = 0;; ++guard) {
     if (guard > 4 * csize + 8) {
-      atomicOr(&X.d.ctl->err, ERR_ALIGN);
+      atomicOr(X.err, ERR_ALIGN);
       return;
     }
     for (int csi = start_csi; csi < csize; ++csi) {
@@ -889,43 +1042,210 @@ __device__ __forceinline__ void multi_ligand_align(const Cx& X) {
   }
 }
 
-// One wave per complex.  The order-dependent sums (periodic shift, centre of
-// mass: BFS member order, main.cpp:1007-1067) are accumulated in member order
-// by every lane from shuffled per-member values, the rigid move is spread
-// over (member, bead) lanes, the lay-down / alignment code (sequential,
-// data-dependent, rare) runs on lane 0, and the members' records are counted
-// in parallel.  Lanes exchange bead values through global memory only after
-// a workgroup-scope fence (the wave's lanes share the CU's L1).
-__device__ __forceinline__ void complex_wave(const KParams& P, const Dev& d, int lb, int lane) {
-  const int p = P.NA + lb;
+// lay-down + alignment on lane 0, main.cpp:1138-1732 (lbB: store index of the
+// root ligand, pA: of the last receptor in member order)
+template <class CX>
+__device__ __forceinline__ void complex_align(const CX& X, int nB, int lbB, int pA) {
+  const KParams& P = X.P;
+  const auto& N = X.N;
+  if (nB == 1) {
+    // lay-down, main.cpp:1140-1193 (exact != test; the receptor is the last
+    // one of the rotation loop, 1107 / 1147)
+    if (N.B(lbB, 1, 2, 2) != (N.B(lbB, 1, 1, 2) + P.rb)) {
+      for (int j = 1; j <= 4; ++j)
+        for (int k = 1; k <= 2; ++k) N.B(lbB, j, k, 2) = N.A(pA, 3, 1, 2);
+      N.B(lbB, 1, 2, 2) = N.A(pA, 3, 1, 2) + P.rb;
+      double angle = kmcm::atan2((N.B(lbB, 2, 1, 0) - N.B(lbB, 1, 1, 0)), (N.B(lbB, 2, 1, 1) - N.B(lbB, 1, 1, 1))) + P.pai;
+      double tx[5][3], ty[5][3];
+      ligand_template(P.rb, tx, ty);
+      double l0x = N.B(lbB, 1, 1, 0), l0y = N.B(lbB, 1, 1, 1);
+      double ca = kmcm::cos(angle), sa = kmcm::sin(angle);
+      for (int j = 1; j <= 4; ++j)
+        for (int k = 1; k <= 2; ++k) {
+          N.B(lbB, j, k, 0) = tx[j][k] * ca - ty[j][k] * sa + l0x;
+          N.B(lbB, j, k, 1) = tx[j][k] * sa + ty[j][k] * ca + l0y;
+        }
+    }
+    // align attached receptors, main.cpp:1196-1233
+    for (int j = 2; j <= 4; ++j) {
+      int a1ref = X.neiB(lbB, j);
+      if (a1ref != 0 && bond_misaligned(P, N, lbB, j, a1ref - 1)) snap_bond(P, N, a1ref - 1, lbB, j, P.bond_cut);
+    }
+    // align their cis partners, main.cpp:1237-1274
+    for (int j = 2; j <= 4; ++j) {
+      int a1ref = X.neiB(lbB, j);
+      if (a1ref != 0 && X.neiA3(a1ref - 1) != 0) {
+        int a1 = a1ref - 1, a2 = X.neiA3(a1) - 1;
+        if (cis_misaligned(P, N, a1, a2)) snap_cis(P, N, a2, a1, P.cis_cut);
+      }
+    }
+  } else if (nB > 1) {
+    multi_ligand_align(X);
+  }
+}
+
+// wave-level ordering of LDS / global accesses between the lanes of one wave
+// (each wave of the complex kernels works on its own complex: no workgroup
+// barrier)
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// LDS image of a complex (lanes < csize): member slots from the BFS row, the
+// links of every member encoded by BFS position (a protein link to member t
+// is t + 1 for a receptor, NA + t + 1 for a ligand; receptor {nei4 (site),
+// nei2, nei3}, ligand {-, nei2, nei3, nei4}).  In three steps so that callers
+// can issue their other loads in the same round: slots (then wave_sync), raw
+// links, encoding.
+__device__ __forceinline__ int cx_stage_slots(const Dev& d, CxLds* L, int off, int csize, int NA, int lane) {
+  int m = -1;
+  if (lane < csize) {
+    m = d.members[off + lane];
+    L->slot[lane] = m;
+    L->res[lane] = m < NA ? lane : NA + lane;
+    L->mv[lane] = 0;
+  }
+  return m;
+}
+__device__ __forceinline__ int3 cx_load_links(const Dev& d, int m, int NA) {
+  const int NB = d.cur.NB;
+  if (m < 0) return make_int3(0, 0, 0);
+  if (m < NA) return make_int3(A_NEI4(d, m), A_NEI2(d, m), A_NEI3(d, m));
+  return make_int3(B_NEI(d, m - NA, 2), B_NEI(d, m - NA, 3), B_NEI(d, m - NA, 4));
+}
+__device__ __forceinline__ void cx_encode_links(const Dev& d, CxLds* L, int m, int3 l, int csize, int NA, int lane) {
+  if (lane >= csize) return;
+  auto enc = [&](int v) -> int {  // slot + 1 -> encoded position + 1 (0 stays 0)
+    if (v <= 0) return 0;
+    for (int t = 0; t < csize; ++t)
+      if (L->slot[t] == v - 1) return (v - 1 < NA ? t : NA + t) + 1;
+    atomicOr(&d.ctl->err, ERR_RESOLVE);  // a link leaving its component
+    return 0;
+  };
+  if (m < NA) {
+    L->lk[lane][0] = l.x;
+    L->lk[lane][1] = enc(l.y);
+    L->lk[lane][2] = enc(l.z);
+  } else {
+    L->lk[lane][1] = enc(l.x);
+    L->lk[lane][2] = enc(l.y);
+    L->lk[lane][3] = enc(l.z);
+  }
+}
+__device__ __forceinline__ void cx_stage_links(const Dev& d, CxLds* L, int off, int csize, int NA, int lane) {
+  const int m = cx_stage_slots(d, L, off, csize, NA, lane);
+  wave_sync();
+  cx_encode_links(d, L, m, cx_load_links(d, m, NA), csize, NA, lane);
+}
+
+// R_new rows of every staged member (paired layout, kmc_device.h), and the
+// member row in its shuffled order (cluster.log, main.cpp:2291-2305)
+__device__ __forceinline__ void cx_write_back(const Dev& d, CxLds* L, int* grow, int csize, int nB, int NA, int lane) {
+  for (int q = 0; q < csize; ++q) {
+    const int m = L->slot[q];
+    const double* b = L->bead[q];
+    if (m < NA) {
+      if (lane < ROWS_A) {
+        double2 v;
+        if (lane < 16) {
+          v = make_double2(b[lane * 3], b[lane * 3 + 1]);
+        } else {
+          const int h = (lane - 16) >> 2, kk = (lane - 16) & 3;
+          v = make_double2(b[((2 * h) * 4 + kk) * 3 + 2], b[((2 * h + 1) * 4 + kk) * 3 + 2]);
+        }
+        d.nxt.A2(m, lane) = v;
+      }
+    } else if (lane < ROWS_B) {
+      double2 v;
+      if (lane < 8) {
+        v = make_double2(b[lane * 3], b[lane * 3 + 1]);
+      } else {
+        const int h = (lane - 8) >> 1, kk = (lane - 8) & 1;
+        v = make_double2(b[((2 * h) * 2 + kk) * 3 + 2], b[((2 * h + 1) * 2 + kk) * 3 + 2]);
+      }
+      d.nxt.B2(m - NA, lane) = v;
+    }
+  }
+  if (nB > 1 && lane < csize) {
+    const int e = L->res[lane];
+    grow[lane] = L->slot[e < NA ? e : e - NA];
+  }
+}
+
+// the old record of member m (lane < csize): its rank in its cell
+__device__ __forceinline__ int cx_count_old(const KParams& P, const Dev& d, int m) {
+  double x, y, zl, zh;
+  ref_point(d, d.cur, m, P.NA, x, y, zl, zh);
+  return atomicAdd(&d.cell_cnt[rec_cell(P, x, y, m >= P.NA)], 1);
+}
+// the staged members' new records (reference point from LDS); rk_old < 0:
+// count the old one here too
+__device__ __forceinline__ void cx_count(const KParams& P, const Dev& d, CxLds* L, int csize, int lane, int rk_old = -1) {
+  if (lane >= csize) return;
+  const int m = L->slot[lane];
+  const double* b = L->bead[lane];
+  const int kind = m >= P.NA;
+  if (rk_old < 0) rk_old = cx_count_old(P, d, m);
+  bool ext = true;
+  for (int j = 2; j <= 4; ++j) {
+    const int o = (kind ? (j - 1) * 2 : (j - 1) * 4) * 3;
+    const double ex = b[o] - b[0], ey = b[o + 1] - b[1];
+    ext &= kind ? ex * ex + ey * ey <= 35.0 * 35.0 : ex * ex + ey * ey <= 0.09;
+  }
+  count_new(P, d, m, rk_old, b[0], b[1], ext);
+}
+
+// Rigid move of one complex, main.cpp:974-1131.  Lane = (member ql of a pass
+// of four, bead slot (j-1)*4 + (k-1)); the order-dependent sums (periodic
+// shift, centre of mass: BFS member order, 994-1067) are accumulated in member
+// order by every lane from shuffled per-member values.  New coordinates go to
+// the LDS image (LDS) or straight to R_new.
+// pass-0 bead of this lane: member ql = lane / 16, bead (lane/4 % 4 + 1, lane % 4 + 1)
+struct Bead0 {
+  double x, y, z;
+  bool ok;
+};
+template <bool LDS>
+__device__ __forceinline__ Bead0 cx_bead0(const KParams& P, const Dev& d, CxLds* L, const int* grow, int csize, int lane) {
+  const int ql = lane >> 4, bj = ((lane >> 2) & 3) + 1, bk = (lane & 3) + 1;
+  Bead0 b{0.0, 0.0, 0.0, false};
+  if (ql < csize) {
+    const int m = LDS ? L->slot[ql] : grow[ql];
+    if (bk <= (m < P.NA ? 4 : 2)) {
+      b.x = d.cur.P(m, bj, bk, 0);
+      b.y = d.cur.P(m, bj, bk, 1);
+      b.z = d.cur.P(m, bj, bk, 2);
+      b.ok = true;
+    }
+  }
+  return b;
+}
+template <bool LDS>
+__device__ __forceinline__ void cx_rigid(const KParams& P, const Dev& d, CxLds* L, const int* grow, int csize, int nB,
+                                         uint32_t rootid, uint32_t step, int lane, Bead0 b0) {
   const int NA = P.NA;
-  const uint32_t step = d.ctl->step;
-  Cx X{P, d, step, p, (uint32_t)d.id_of[p], d.members + d.cx_off[lb], d.cx_size[lb]};
-  const int* res = X.res;
-  const int csize = X.size;
-  const int nB = d.cx_nb[lb], nA = csize - nB;
-  // rigid move, main.cpp:974-1131
+  const int nA = csize - nB;
+  auto mslot = [&](int q) { return LDS ? L->slot[q] : grow[q]; };
   double u0, u1, u2, u3;
-  kmcr::uniform2(P.key, kmcr::DOM_DIFF, X.rootid, 0, step, 0, &u0, &u1);
-  kmcr::uniform2(P.key, kmcr::DOM_DIFF, X.rootid, 0, step, 1, &u2, &u3);
+  kmcr::uniform2(P.key, kmcr::DOM_DIFF, rootid, 0, step, 0, &u0, &u1);
+  kmcr::uniform2(P.key, kmcr::DOM_DIFF, rootid, 0, step, 1, &u2, &u3);
   double amp = (nB == 1 ? P.amp_bond : 0.0) * u0;
   double phai = u1 * 2 * P.pai;
   double dx = amp * kmcm::cos(phai), dy = amp * kmcm::sin(phai);
-  // lane = (member ql of a pass of four, bead slot (j-1)*4 + (k-1)); the
-  // first pass's beads stay in registers (most complexes have <= 4 members)
   const int ql = lane >> 4, bj = ((lane >> 2) & 3) + 1, bk = (lane & 3) + 1;
   const int npass = (csize + 3) >> 2;
-  double c0x = 0, c0y = 0, c0z = 0;
-  bool c0 = false;
-  if (ql < csize) {
-    const int m = res[ql];
-    c0 = bk <= X.nk(m);
-    if (c0) {
-      c0x = X.R(m, bj, bk, 0);
-      c0y = X.R(m, bj, bk, 1);
-      c0z = X.R(m, bj, bk, 2);
-    }
-  }
+  auto load = [&](int q, double& x, double& y, double& z) -> bool {
+    if (q >= csize) return false;
+    const int m = mslot(q);
+    if (bk > (m < NA ? 4 : 2)) return false;
+    x = d.cur.P(m, bj, bk, 0);
+    y = d.cur.P(m, bj, bk, 1);
+    z = d.cur.P(m, bj, bk, 2);
+    return true;
+  };
+  const double c0x = b0.x, c0y = b0.y, c0z = b0.z;
+  const bool c0 = b0.ok;
   // bead of this lane in pass ps: valid?, R coordinates
   auto bead = [&](int ps, double& x, double& y, double& z) -> bool {
     if (ps == 0) {
@@ -934,14 +1254,7 @@ __device__ __forceinline__ void complex_wave(const KParams& P, const Dev& d, int
       z = c0z;
       return c0;
     }
-    const int q = ps * 4 + ql;
-    if (q >= csize) return false;
-    const int m = res[q];
-    if (bk > X.nk(m)) return false;
-    x = X.R(m, bj, bk, 0);
-    y = X.R(m, bj, bk, 1);
-    z = X.R(m, bj, bk, 2);
-    return true;
+    return load(ps * 4 + ql, x, y, z);
   };
   // periodic shift from the members' [1][1] in member order (main.cpp:994-1004)
   double PBx = 0, PBy = 0;
@@ -979,91 +1292,165 @@ __device__ __forceinline__ void complex_wave(const KParams& P, const Dev& d, int
   for (int ps = 0; ps < npass; ++ps) {
     double x = 0, y = 0, z = 0;
     if (!bead(ps, x, y, z)) continue;
-    const int m = res[ps * 4 + ql];
+    const int q = ps * 4 + ql, m = mslot(q);
     double ox = (x + dx) - PBx;
     double oy = (y + dy) - PBy;
     double oz = z;
-    X.N(m, bj, bk, 0) = rx(t, ox, oy, oz, cmx, cmy, cmz);
-    X.N(m, bj, bk, 1) = ry(t, ox, oy, oz, cmx, cmy, cmz);
-    X.N(m, bj, bk, 2) = rz(t, ox, oy, oz, cmx, cmy, cmz);
+    const double nx = rx(t, ox, oy, oz, cmx, cmy, cmz), ny = ry(t, ox, oy, oz, cmx, cmy, cmz),
+                 nz = rz(t, ox, oy, oz, cmx, cmy, cmz);
+    if (LDS) {
+      double* b = &L->bead[q][((bj - 1) * (m < NA ? 4 : 2) + (bk - 1)) * 3];
+      b[0] = nx;
+      b[1] = ny;
+      b[2] = nz;
+    } else {
+      d.nxt.P(m, bj, bk, 0) = nx;
+      d.nxt.P(m, bj, bk, 1) = ny;
+      d.nxt.P(m, bj, bk, 2) = nz;
+    }
   }
-  int pA = -1;  // last receptor in member order (the lay-down's receptor)
-  for (int base = 0; base < csize; base += 64) {
-    const int t2 = base + lane;
-    const int m = t2 < csize ? res[t2] : -1;
-    const uint64_t am = __ballot(t2 < csize && m < NA);
-    if (am) pA = __shfl(m, 63 - __clzll((long long)am), 64);
-  }
-  __threadfence_block();
-  if (lane == 0) {
-    const Beads& N = d.nxt;
-    if (nB == 1) {
-      const int lbB = lb;  // the only ligand is the root
-      // lay-down, main.cpp:1140-1193 (exact != test)
-      if (N.B(lbB, 1, 2, 2) != (N.B(lbB, 1, 1, 2) + P.rb)) {
-        for (int j = 1; j <= 4; ++j)
-          for (int k = 1; k <= 2; ++k) N.B(lbB, j, k, 2) = N.A(pA, 3, 1, 2);
-        N.B(lbB, 1, 2, 2) = N.A(pA, 3, 1, 2) + P.rb;
-        double angle = kmcm::atan2((N.B(lbB, 2, 1, 0) - N.B(lbB, 1, 1, 0)), (N.B(lbB, 2, 1, 1) - N.B(lbB, 1, 1, 1))) + P.pai;
-        double tx[5][3], ty[5][3];
-        ligand_template(P.rb, tx, ty);
-        double l0x = N.B(lbB, 1, 1, 0), l0y = N.B(lbB, 1, 1, 1);
-        double ca = kmcm::cos(angle), sa = kmcm::sin(angle);
-        for (int j = 1; j <= 4; ++j)
-          for (int k = 1; k <= 2; ++k) {
-            N.B(lbB, j, k, 0) = tx[j][k] * ca - ty[j][k] * sa + l0x;
-            N.B(lbB, j, k, 1) = tx[j][k] * sa + ty[j][k] * ca + l0y;
-          }
-      }
-      // align attached receptors, main.cpp:1196-1233
-      for (int j = 2; j <= 4; ++j) {
-        int a1ref = X.neiB(lbB, j);
-        if (a1ref != 0 && bond_misaligned(P, N, lbB, j, a1ref - 1)) snap_bond(P, N, a1ref - 1, lbB, j, P.bond_cut);
-      }
-      // align their cis partners, main.cpp:1237-1274
-      for (int j = 2; j <= 4; ++j) {
-        int a1ref = X.neiB(lbB, j);
-        if (a1ref != 0 && X.neiA3(a1ref - 1) != 0) {
-          int a1 = a1ref - 1, a2 = X.neiA3(a1) - 1;
-          if (cis_misaligned(P, N, a1, a2)) snap_cis(P, N, a2, a1, P.cis_cut);
+}
+
+// k_complex: one wave per complex of up to CXL members, grid-stride over
+// cx_list (a shared dispatch counter would serialise one atomic per complex).
+// The member records and the moved beads live in LDS.  The lay-down /
+// alignment code (main.cpp:1138-1732) changes nothing when every one of its
+// tests passes — a single ligand already laid down (1141), its receptors on
+// their sites (1215) and their cis partners on theirs (1255); these tests are
+// independent when nothing moves, so lanes 0-3 evaluate them in parallel.
+// A complex that passes is written back and its records counted here; any
+// other (a test fails, or several ligands: the shuffled multi-ligand passes)
+// is written back as moved and handed to k_complex_heavy, so the register-
+// heavy sequential code stays out of this kernel (occupancy).
+__global__ void __launch_bounds__(256) k_complex(KParams P, Dev d) {
+  __shared__ CxLds lds[4];
+  const int lane = __lane_id(), NA = P.NA;
+  CxLds* L = &lds[threadIdx.x >> 6];
+  const uint32_t n = d.ctl->n_cx, step = d.ctl->step;
+  const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+  Stamper S(16);
+  int4 next = w < n ? d.cx_list[w] : make_int4(0, 0, 0, 0);
+  for (uint32_t c = w; c < n; c += nw) {
+    const int4 desc = next;
+    if (c + nw < n) next = d.cx_list[c + nw];  // prefetch the wave's next descriptor
+    const int csize = desc.z & 0xffff, nB = desc.z >> 16;
+    S(d, 5);
+    const int m = cx_stage_slots(d, L, desc.y, csize, NA, lane);
+    wave_sync();
+    // one round of independent loads: the lane's pass-0 bead, its member's
+    // links and old reference point (whose record rank is taken right away)
+    const Bead0 b0 = cx_bead0<true>(P, d, L, nullptr, csize, lane);
+    const int3 lk = cx_load_links(d, m, NA);
+    const int rk_old = m >= 0 ? cx_count_old(P, d, m) : 0;
+    cx_encode_links(d, L, m, lk, csize, NA, lane);
+    S(d, 0);
+    cx_rigid<true>(P, d, L, nullptr, csize, nB, (uint32_t)desc.w, step, lane, b0);
+    wave_sync();
+    S(d, 1);
+    bool bad = false;
+    if (nB == 1 && lane < 4) {  // the root is member 0, the complex's only ligand
+      const LdsBeads N{L};
+      if (lane == 0) {
+        bad = N.B(0, 1, 2, 2) != (N.B(0, 1, 1, 2) + P.rb);
+      } else {
+        const int j = lane + 1, a1ref = L->lk[0][j - 1];
+        if (a1ref != 0) {
+          const int a1 = a1ref - 1, a2ref = L->lk[a1][2];
+          bad = bond_misaligned(P, N, 0, j, a1) || (a2ref != 0 && cis_misaligned(P, N, a1, a2ref - 1));
         }
       }
     }
-    if (nB > 1) multi_ligand_align(X);
+    const bool heavy = nB != 1 || __ballot(bad) != 0;
+    S(d, 2);
+    cx_write_back(d, L, nullptr, csize, 1, NA, lane);
+    S(d, 3);
+    if (heavy) {
+      // k_complex_heavy counts the new records; the old ranks are kept
+      if (lane < csize) d.rank[m] = make_int2(rk_old, -1);
+      if (lane == 0) d.cx_heavy[atomicAdd(&d.ctl->n_heavy, 1u)] = make_int4(desc.x | CXD_MOVED, desc.y, desc.z, desc.w);
+    } else {
+      cx_count(P, d, L, csize, lane, rk_old);
+    }
+    wave_sync();
+    S(d, 4);
   }
-  __threadfence_block();
-  for (int t2 = lane; t2 < csize; t2 += 64) count_records(P, d, res[t2]);
 }
 
-// nblk workgroups; each wave takes complexes from the BFS's root list.
-// Wave 0 first runs the BFS of the components that overflowed k_bfs's
-// register queue (rare: > BFS_QCAP members) and moves those it roots.
-__device__ __forceinline__ void complex_waves(const KParams& P, const Dev& d, int blk, int nblk) {
-  const int w = blk * (blockDim.x >> 6) + (threadIdx.x >> 6), nw = nblk * (blockDim.x >> 6);
-  const uint32_t n = d.ctl->n_cx;
-  if (w == 0) {
+// k_complex_heavy: the complexes k_complex did not finish.  Staged ones (<=
+// CXL members, already moved) are reloaded from R_new into LDS and lane 0
+// runs the lay-down / alignment code against LDS; larger ones run the rigid
+// move and the alignment on global memory.  Block 0's first wave first runs
+// the BFS of the components that overflowed k_bfs's LDS queue (> BFS_QCAP
+// members) and moves those it roots.  Launched after k_complex on its stream.
+__global__ void __launch_bounds__(256) k_complex_heavy(KParams P, Dev d) {
+  __shared__ CxLds lds[4];
+  const int lane = __lane_id(), NA = P.NA, NB = P.NB;
+  CxLds* L = &lds[threadIdx.x >> 6];
+  const uint32_t step = d.ctl->step;
+  auto global_path = [&](int lb) {
+    int* grow = d.members + d.cx_off[lb];
+    const int csize = d.cx_size[lb], nB = d.cx_nb[lb];
+    cx_rigid<false>(P, d, L, grow, csize, nB, (uint32_t)d.id_of[NA + lb], step, lane,
+                    cx_bead0<false>(P, d, L, grow, csize, lane));
+    wave_sync();
+    if (lane == 0) {
+      int pA = -1;  // last receptor in member order (main.cpp:1107, 1147)
+      for (int q = csize - 1; q >= 0 && pA < 0; --q)
+        if (grow[q] < NA) pA = grow[q];
+      CxT<Beads, GlbLinks> X{P, step, (uint32_t)d.id_of[NA + lb], grow, csize, d.nxt, GlbLinks{&d, NA, NB, step},
+                             &d.ctl->err};
+      complex_align(X, nB, lb, pA);
+    }
+    wave_sync();
+    for (int q = lane; q < csize; q += 64) count_records(P, d, grow[q]);
+  };
+  if (blockIdx.x == 0 && threadIdx.x < 64) {
     const uint32_t no = d.ctl->n_overflow;
     for (uint32_t o = 0; o < no; ++o) {
-      int lb = __lane_id() == 0 ? bfs_overflow_one(P, d, o) : -1;
+      int lb = lane == 0 ? bfs_overflow_one(P, d, o) : -1;
       lb = __shfl(lb, 0, 64);
-      __threadfence_block();
-      if (lb >= 0) complex_wave(P, d, lb, __lane_id());
+      wave_sync();
+      if (lb >= 0) global_path(lb);
     }
   }
-  for (uint32_t c = w; c < n; c += nw) complex_wave(P, d, d.cx_list[c], __lane_id());
-}
-// Complexes (the first cx_blocks workgroups, dispatched first; 0 without
-// ligands) and the free units (the rest, one thread per slot) in one launch:
-// the complexes' latency-bound waves overlap the free units' HBM stream
-// (measured 0.514 -> 0.494 ms/step at C3 against two launches; a side stream
-// was slower).  The two sets of proteins are disjoint and the record counts
-// are commutative atomics.
-__global__ void __launch_bounds__(256) k_propose(KParams P, Dev d) {
-  if ((int)blockIdx.x < P.cx_blocks) {
-    complex_waves(P, d, blockIdx.x, P.cx_blocks);
-    return;
+  const uint32_t n = d.ctl->n_heavy;
+  const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+  for (uint32_t c = w; c < n; c += nw) {
+    const int4 desc = d.cx_heavy[c];
+    const int lb = desc.x & CXD_LB;
+    if (!(desc.x & CXD_MOVED)) {
+      global_path(lb);
+      continue;
+    }
+    const int csize = desc.z & 0xffff, nB = desc.z >> 16;
+    cx_stage_links(d, L, desc.y, csize, NA, lane);
+    wave_sync();
+    for (int e = lane; e < csize * 16; e += 64) {  // the moved beads back into LDS
+      const int q = e >> 4, m = L->slot[q], bj = ((e >> 2) & 3) + 1, bk = (e & 3) + 1;
+      if (bk > (m < NA ? 4 : 2)) continue;
+      double* b = &L->bead[q][((bj - 1) * (m < NA ? 4 : 2) + (bk - 1)) * 3];
+      b[0] = d.nxt.P(m, bj, bk, 0);
+      b[1] = d.nxt.P(m, bj, bk, 1);
+      b[2] = d.nxt.P(m, bj, bk, 2);
+    }
+    wave_sync();
+    if (lane == 0) {
+      int pA = -1;  // last receptor in member order
+      for (int q = csize - 1; q >= 0 && pA < 0; --q)
+        if (L->slot[q] < NA) pA = q;
+      CxT<LdsBeads, LdsLinks> X{P, step, (uint32_t)desc.w, L->res, csize, LdsBeads{L}, LdsLinks{L, NA}, &d.ctl->err};
+      complex_align(X, nB, 0, pA);  // the root is member 0
+    }
+    wave_sync();
+    cx_write_back(d, L, d.members + desc.y, csize, nB, NA, lane);
+    cx_count(P, d, L, csize, lane, lane < csize ? d.rank[L->slot[lane]].x : 0);  // old rank: k_complex
+    wave_sync();
   }
-  propose_one(P, d, ((int)blockIdx.x - P.cx_blocks) * blockDim.x + threadIdx.x);
+}
+
+// free units (free receptors, cis dimers, free ligands), one thread per slot
+__global__ void __launch_bounds__(256) k_propose_free(KParams P, Dev d) {
+  propose_one(P, d, (int)(blockIdx.x * blockDim.x + threadIdx.x));
 }
 
 #define RID_PID 0x00ffffff
@@ -1214,18 +1601,6 @@ struct WgList {
   uint32_t base;
 };
 
-// slot for each calling lane (call from the lanes that emit)
-__device__ __forceinline__ uint32_t wave_slot(uint32_t* ctr) {
-  const uint64_t mask = __ballot(1);
-  const int lane = __lane_id();
-  const int leader = __ffsll((unsigned long long)mask) - 1;
-  const uint32_t rank = __popcll(mask & ((1ull << lane) - 1ull));
-  uint32_t base = 0;
-  if (lane == leader) base = atomicAdd(ctr, (uint32_t)__popcll(mask));
-  base = __shfl(base, leader, 64);
-  return base + rank;
-}
-
 __device__ __forceinline__ void wg_list_init(WgList& L) {
   if (threadIdx.x == 0) L.n = 0;
   __syncthreads();
@@ -1306,34 +1681,6 @@ __device__ __forceinline__ void wg_flush(WgList& L, const SList& out, uint32_t* 
     else atomicOr(err, ERR_EDGES);
   }
 }
-
-// ---------------------------------------------------------------- stamps
-// Diagnostic build only (-DKMC_STAMPS): thread 0 of each workgroup adds the
-// cycles since its previous stamp to ctl->stamps[base + i] (phase shares of
-// the tile scans; kmc_step prints them with KMC_DEBUG_COUNTS=1).  In the
-// real build a stamp compiles to nothing.
-struct Stamper {
-#ifdef KMC_STAMPS
-  uint64_t t;
-  int base;
-  __device__ static uint64_t now() {
-    uint64_t v;
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");
-    return v;
-  }
-  __device__ explicit Stamper(int b) : t(now()), base(b) {}
-  __device__ void operator()(const Dev& d, int i) {
-    if (threadIdx.x == 0) {
-      const uint64_t v = now();
-      atomicAdd((unsigned long long*)&d.ctl->stamps[base + i], (unsigned long long)(v - t));
-      t = v;
-    }
-  }
-#else
-  __device__ explicit Stamper(int) {}
-  __device__ void operator()(const Dev&, int) {}
-#endif
-};
 
 // ---------------------------------------------------------------- LDS tiles
 // Records are sorted by (cell row, kind, cell column) — cell_index() — so the
@@ -2371,6 +2718,7 @@ __global__ void __launch_bounds__(256) k_finalize(KParams P, Dev d, double time_
   c->n_overflow = 0;
   c->cx_cursor = 0;
   c->n_cx = 0;
+  c->n_heavy = 0;
   c->n_pend = 0;
   c->n_rl = 0;
   c->n_cisc = 0;
@@ -2391,11 +2739,25 @@ __device__ __forceinline__ uint32_t slot_key(const KParams& P, double x, double 
   return ((uint32_t)((cy / t) * ntx + cx / t) * t + (uint32_t)(cy % t)) * t + (uint32_t)(cx % t);
 }
 
-__global__ void k_slot_keys(KParams P, Dev d, uint32_t* keys, int32_t* vals) {
+// Sort key of slot s: (cell << 32) | unit.  With grouping, a protein takes
+// the cell of its unit's lead (the last step's owner key: a complex's root
+// ligand, a cis dimer's lead receptor, else itself) and the lead's reference
+// index as the low word, so the members of one unit occupy consecutive slots
+// of their kind: the complex kernels then touch a few cache lines per bead
+// row instead of one per member.
+__global__ void k_slot_keys(KParams P, Dev d, uint64_t* keys, int32_t* vals, bool group) {
   int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= P.N) return;
-  double x = d.cur.P(s, 1, 1, 0), y = d.cur.P(s, 1, 1, 1);
-  keys[s] = slot_key(P, x, y);
+  int lead = s, own = d.id_of[s];
+  if (group) {
+    const int o = d.owner[s];
+    if (o >= 0 && o < P.N) {
+      lead = d.slot_of[o];
+      own = o;
+    }
+  }
+  double x = d.cur.P(lead, 1, 1, 0), y = d.cur.P(lead, 1, 1, 1);
+  keys[s] = (uint64_t)slot_key(P, x, y) << 32 | (uint32_t)(group ? own : 0);
   vals[s] = s < P.NA ? s : s - P.NA;
 }
 
