@@ -41,11 +41,12 @@ struct Ctl {
   uint32_t err_step;      // first step whose kernels raised an error bit (k_finalize), 0 = none
   // per-step work-list counters
   uint32_t n_overflow;    // ligands whose BFS overflowed the register queue
-  uint32_t cx_cursor;     // members[] allocation cursor
+  uint32_t cx_cursor;     // members[] allocation cursor (rows are kept across steps; k_cx_kill resets)
   uint32_t n_pend;        // units still pending after a round (pass C)
   uint32_t n_cx;          // complexes registered by the BFS this step (cx_list)
   uint32_t n_heavy;       // entries of cx_heavy this step
-  uint32_t pad1;
+  uint32_t full_now;      // k_cx_kill: no complex kept this step (every bonded ligand runs the BFS)
+  uint32_t n_dirty[2];    // proteins whose bonds changed during step s: list s & 1
   uint32_t last[8];       // previous step's work counts (diagnostics): cand conf plist rej pairs rl cisc overflow
   uint32_t n_rl;          // R–L accepting edges
   uint32_t n_cisc;        // cis candidates

@@ -19,12 +19,12 @@ using namespace kmcd;
 
 // kernel ids for per-kernel HIP-event timing (kmc_set_timing / kmc_kernel_times)
 enum KId {
-  KI_CLASSIFY, KI_BFS, KI_PROPOSE, KI_PROPOSE_FREE, KI_COMPLEX, KI_CX_HEAVY, KI_SCAN, KI_REC_SCATTER,
+  KI_CLASSIFY, KI_BFS, KI_PROPOSE, KI_PROPOSE_FREE, KI_COMPLEX, KI_CX_HEAVY, KI_CX_KILL, KI_SCAN, KI_REC_SCATTER,
   KI_COL_SCAN, KI_COL_EXACT, KI_COL_ROUNDS, KI_COMMIT, KI_RXN_SCAN, KI_RXN_EXACT, KI_MATCH, KI_DISS_OBSERVE,
   KI_RESORT, KI_N
 };
 static const char* const KNAMES[KI_N] = {
-    "k_classify", "k_bfs", "k_propose", "k_propose_free", "k_complex", "k_complex_heavy", "k_scan",
+    "k_classify", "k_bfs", "k_propose", "k_propose_free", "k_complex", "k_complex_heavy", "k_cx_kill", "k_scan",
     "k_rec_scatter", "k_col_scan", "k_col_exact", "k_col_rounds", "k_commit", "k_rxn_scan", "k_rxn_exact",
     "k_match", "k_diss_observe", "slot_resort"};
 #define TRING 64  // steps of event pairs kept in flight
@@ -60,6 +60,10 @@ struct kmc_sim {
   int32_t *snap_ai = nullptr, *snap_bi = nullptr, *snap_id = nullptr, *snap_slot = nullptr;
   Ctl* snap_ctl = nullptr;
   int64_t n_replays = 0;
+  // complexes are kept across steps (k_cx_kill); full: register every one anew
+  // at the next step (set after a new state, a re-sort is handled per step, an
+  // undone chunk); KMC_FULL_BFS=1: every step
+  bool need_full = true, always_full = false;
   bool debug_counts = false;  // KMC_DEBUG_COUNTS=1: print the last step's work counts per kmc_step chunk
   // slot order (kmc_kernels.hip §slot order): scratch of the re-sort
   int64_t resort_every = 100, since_resort = 0;
@@ -291,7 +295,14 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   rc |= dalloc(s, &d.cx_off, NB);
   rc |= dalloc(s, &d.cx_size, NB);
   rc |= dalloc(s, &d.cx_nb, NB);
-  rc |= dalloc(s, &d.members, N);
+  d.mcap = (uint32_t)(3 * (size_t)N);
+  rc |= dalloc(s, &d.members, d.mcap);
+  rc |= dalloc(s, &d.shuf, d.mcap);
+  rc |= dalloc(s, &d.shuf_tag, NB);
+  rc |= dalloc(s, &d.croot, N);
+  rc |= dalloc(s, &d.cx_alive, NB);
+  rc |= dalloc(s, &d.bfs_cand, NB);
+  rc |= dalloc(s, &d.dlist, 2 * (size_t)N);
   rc |= dalloc(s, &d.pend, N);
   rc |= dalloc(s, &d.overflow, NB);
   rc |= dalloc(s, &d.cx_list, NB);
@@ -338,6 +349,8 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
     if (te && *te) t = std::max(2, std::min(TILE_MAX, atoi(te)));
     K.tile = t;
     // k_complex waves: up to one per 4 ligands, at most 4096
+    const char* fb = getenv("KMC_FULL_BFS");
+    s->always_full = fb && *fb == '1';
     const char* cm = getenv("KMC_CX_MODE");
     if (cm && *cm) s->cx_mode = std::max(1, std::min(4, atoi(cm)));
     // k_complex: enough 4-wave workgroups to fill every CU (dynamic dispatch:
@@ -574,6 +587,7 @@ int kmc_set_state(kmc_sim* s, const kmc_state_view* v) {
   s->step_done = v->step;
   s->since_resort = 0;
   s->have_state = true;
+  s->need_full = true;
   return KMC_OK;
 }
 
@@ -716,6 +730,11 @@ static int launch_step(kmc_sim* s, bool re_sort) {
     (void)hipMemsetAsync(d.nxt.a, 0xff, sizeof(double) * 48 * (size_t)K.NA, st);
     (void)hipMemsetAsync(d.nxt.b, 0xff, sizeof(double) * 24 * (size_t)K.NB, st);
   }
+  if (K.NB > 0) {
+    const int full = (s->need_full || re_sort || s->always_full) ? 1 : 0;
+    s->need_full = false;
+    TIMED(KI_CX_KILL, (k_cx_kill<<<std::min(gN, 1024), T, 0, st>>>(K, d, full)));
+  }
   TIMED(KI_CLASSIFY, (k_classify<<<gN, T, 0, st>>>(K, d)));
   if (s->cx_mode == 4 && K.NB > 0) {
     // the complex chain (BFS, moves, heavy path) on the side stream beside the
@@ -847,6 +866,7 @@ int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out) {
       rc = snapshot(s, true);
       if (rc != KMC_OK) return rc;
       s->since_resort = since0;
+      s->need_full = true;  // the kept complexes may describe the undone steps
       ++s->n_replays;
       if (err == ERR_EDGES && s->grow < 6) {  // at most 64x the default lists
         s->grow += 1;
@@ -941,7 +961,12 @@ int kmc_get_clusters(kmc_sim* s, int32_t* row_len, int32_t* members) {
   HIPCHK(s, hipMemcpy(kind.data(), s->d.ukind, N, hipMemcpyDeviceToHost));
   HIPCHK(s, hipMemcpy(off.data(), s->d.cx_off, sizeof(int32_t) * NB, hipMemcpyDeviceToHost));
   HIPCHK(s, hipMemcpy(size.data(), s->d.cx_size, sizeof(int32_t) * NB, hipMemcpyDeviceToHost));
-  HIPCHK(s, hipMemcpy(mem.data(), s->d.members, sizeof(int32_t) * N, hipMemcpyDeviceToHost));
+  std::vector<int32_t> shuf(s->d.mcap);
+  std::vector<uint32_t> stag(NB);
+  mem.resize(s->d.mcap);
+  HIPCHK(s, hipMemcpy(mem.data(), s->d.members, sizeof(int32_t) * s->d.mcap, hipMemcpyDeviceToHost));
+  HIPCHK(s, hipMemcpy(shuf.data(), s->d.shuf, sizeof(int32_t) * s->d.mcap, hipMemcpyDeviceToHost));
+  HIPCHK(s, hipMemcpy(stag.data(), s->d.shuf_tag, sizeof(uint32_t) * NB, hipMemcpyDeviceToHost));
   HIPCHK(s, hipMemcpy(id_of.data(), s->d.id_of, sizeof(int32_t) * N, hipMemcpyDeviceToHost));
   HIPCHK(s, hipMemcpy(slot_of.data(), s->d.slot_of, sizeof(int32_t) * N, hipMemcpyDeviceToHost));
   // unit tables of the last step's classification (slots are re-sorted only
@@ -955,7 +980,9 @@ int kmc_get_clusters(kmc_sim* s, int32_t* row_len, int32_t* members) {
     } else if (kind[p] == U_COMPLEX) {
       int lb = p - NA;
       row_len[b] = size[lb];
-      for (int t = 0; t < size[lb]; ++t) members[o++] = id_of[mem[off[lb] + t]] + 1;
+      // the row after the multi-ligand shuffles when this step shuffled it
+      const int32_t* row = (stag[lb] == (uint32_t)s->step_done ? shuf.data() : mem.data()) + off[lb];
+      for (int t = 0; t < size[lb]; ++t) members[o++] = id_of[row[t]] + 1;
     } else {
       row_len[b] = 0;
     }

@@ -53,7 +53,14 @@ struct Dev {
   int32_t* cx_off;   // [NB]
   int32_t* cx_size;  // [NB]
   int32_t* cx_nb;    // [NB] ligands in complex
-  int32_t* members;  // [N]
+  int32_t* members;  // [mcap] BFS rows of the registered complexes (kept across steps, BFS order)
+  int32_t* shuf;     // [mcap] the rows after this step's multi-ligand shuffles (cluster.log)
+  uint32_t* shuf_tag;  // [NB] step whose shuffled row of root lb is in shuf
+  uint32_t mcap;     // members[] capacity (3N): rows are appended until a full rebuild
+  int32_t* croot;    // [N] slot of the root ligand of the protein's registered complex, -1 none
+  uint32_t* cx_alive;  // [NB] 1 while ligand lb roots a registered complex
+  uint32_t* bfs_cand;  // [NB] step tag: ligand lb runs the BFS this step
+  int32_t* dlist;    // [2][N] proteins whose bonds changed during step s (list s & 1)
   uint32_t* pend;    // [N] round tag: unit still waiting (resolution pass C)
   int32_t* overflow; // [NB]
   int4* cx_list;     // [NB] descriptors of this step's complexes of <= CXL members (k_complex)
@@ -128,64 +135,7 @@ __device__ __forceinline__ int cell_y(const KParams& P, double y) {
   return c < 0 ? 0 : (c >= P.ncy ? P.ncy - 1 : c);
 }
 
-// ================================================================ 1. classify
-// Unit kinds, main.cpp:584 (free receptor), 682-686 (cis dimer, moved at the
-// lower index), 905 (single ligand = BFS component of size 1).
-__global__ void k_classify(KParams P, Dev d) {
-  const int NA = P.NA, NB = P.NB;
-  int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= P.N) return;
-  uint8_t kind = U_NONE;
-  int own = -1;
-  if (p < NA) {
-    int i = p;
-    int n2 = A_NEI2(d, i), n3 = A_NEI3(d, i);
-    if (A_ST2(d, i) == 0 && A_ST3(d, i) == 0) {
-      kind = U_FREE_A;
-      own = p;
-    } else if (n2 == 0 && n3 != 0 && A_NEI3(d, n3 - 1) == i + 1 && A_NEI2(d, n3 - 1) == 0) {
-      int q = n3 - 1;
-      const bool lead = d.id_of[i] < d.id_of[q];  // moved at the lower reference index
-      own = lead ? i : q;
-      kind = lead ? U_DIMER : U_NONE;
-    }
-  } else {
-    int b = p - NA;
-    if (B_NEI(d, b, 2) == 0 && B_NEI(d, b, 3) == 0 && B_NEI(d, b, 4) == 0) {
-      kind = U_FREE_B;
-      own = p;
-    }
-  }
-  d.ukind[p] = kind;
-  d.owner[p] = own < 0 ? -1 : d.id_of[own];  // -1: complex member, set by the BFS kernels
-}
-
-// ================================================================ BFS
-// Complex of ligand root b: BFS over the bond graph exactly as
-// main.cpp:525-561 (receptor neighbours res_nei[2], [3]; ligand neighbours
-// res_nei[2], [3], [4]; a node is enqueued when first seen).  The root is the
-// lowest-indexed ligand of its component; the BFS of any other ligand of the
-// component finds a lower one among its members and registers nothing.
-#define BFS_QCAP 32
-#define BFS_BATCH 4
 #define CXL 16  // members of a complex staged in LDS by k_complex (see §complexes)
-
-// the neighbours in three fixed slots (-1 = none), in BFS order
-__device__ __forceinline__ void nbrs3(const KParams& P, const Dev& d, int x, int* y) {
-  const int NA = P.NA, NB = P.NB;
-  if (x < NA) {
-    const int a = A_NEI2(d, x), b = A_NEI3(d, x);
-    y[0] = a > 0 ? a - 1 : (b > 0 ? b - 1 : -1);
-    y[1] = a > 0 && b > 0 ? b - 1 : -1;
-    y[2] = -1;
-  } else {
-    const int lb = x - NA;
-    const int v2 = B_NEI(d, lb, 2), v3 = B_NEI(d, lb, 3), v4 = B_NEI(d, lb, 4);
-    y[0] = v2 > 0 ? v2 - 1 : -1;
-    y[1] = v3 > 0 ? v3 - 1 : -1;
-    y[2] = v4 > 0 ? v4 - 1 : -1;
-  }
-}
 
 // slot for each calling lane (call from the lanes that emit)
 __device__ __forceinline__ uint32_t wave_slot(uint32_t* ctr) {
@@ -217,6 +167,124 @@ __device__ __forceinline__ uint32_t wave_alloc(uint32_t* ctr, uint32_t qn) {
   return (uint32_t)__shfl((int)base, leader, 64) + pre;
 }
 
+// ================================================================ 1. classify
+// Unit kinds, main.cpp:584 (free receptor), 682-686 (cis dimer, moved at the
+// lower index), 905 (single ligand = BFS component of size 1).
+__global__ void k_classify(KParams P, Dev d) {
+  const int NA = P.NA, NB = P.NB;
+  int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P.N) return;
+  uint8_t kind = U_NONE;
+  int own = -1;
+  if (p < NA) {
+    int i = p;
+    int n2 = A_NEI2(d, i), n3 = A_NEI3(d, i);
+    if (A_ST2(d, i) == 0 && A_ST3(d, i) == 0) {
+      kind = U_FREE_A;
+      own = p;
+    } else if (n2 == 0 && n3 != 0 && A_NEI3(d, n3 - 1) == i + 1 && A_NEI2(d, n3 - 1) == 0) {
+      int q = n3 - 1;
+      const bool lead = d.id_of[i] < d.id_of[q];  // moved at the lower reference index
+      own = lead ? i : q;
+      kind = lead ? U_DIMER : U_NONE;
+    }
+  } else {
+    int b = p - NA;
+    if (B_NEI(d, b, 2) == 0 && B_NEI(d, b, 3) == 0 && B_NEI(d, b, 4) == 0) {
+      kind = U_FREE_B;
+      own = p;
+    }
+  }
+  // a member of a complex registered in an earlier step and untouched since
+  // (k_cx_kill): its unit is that complex; its root lists it for the complex
+  // kernels (new complexes are registered and listed by k_bfs)
+  const int r = d.croot[p];
+  if (r >= 0) {
+    own = r;
+    if (r == p) {
+      kind = U_COMPLEX;
+      const int b = p - NA, off = d.cx_off[b], sz = d.cx_size[b], nb = d.cx_nb[b];
+      const int4 desc = make_int4(b, off, sz | nb << 16, d.id_of[p]);
+      if (sz <= CXL) d.cx_list[wave_slot(&d.ctl->n_cx)] = desc;
+      else d.cx_heavy[wave_slot(&d.ctl->n_heavy)] = desc;
+    }
+  }
+  d.ukind[p] = kind;
+  d.owner[p] = own < 0 ? -1 : d.id_of[own];  // -1: member of a complex k_bfs registers this step
+}
+
+// Complexes are kept from step to step: a BFS row depends only on the bond
+// graph, which changes only where a bond formed or broke (k_match,
+// k_diss_observe list those proteins).  Before classification, every
+// complex containing a listed protein is dissolved (its members' croot
+// reset) and its ligands, and the listed ligands, become BFS candidates; the
+// BFS of the candidates (k_bfs) registers the new complexes.  full: no
+// complex is kept (after a re-sort, a new state, an undone chunk — or when the
+// appended rows fill half of members[]): every bonded ligand runs the BFS.
+__global__ void k_cx_kill(KParams P, Dev d, int full) {
+  const int NA = P.NA;
+  const uint32_t step = d.ctl->step;
+  full |= d.ctl->cx_cursor > d.mcap / 2;
+  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, nt = gridDim.x * blockDim.x;
+  if (full) {
+    for (uint32_t p = tid; p < (uint32_t)P.N; p += nt) d.croot[p] = -1;
+    for (uint32_t b = tid; b < (uint32_t)P.NB; b += nt) d.cx_alive[b] = 0;
+    if (tid == 0) {
+      d.ctl->cx_cursor = 0;
+      d.ctl->full_now = 1;
+    }
+    return;
+  }
+  if (tid == 0) d.ctl->full_now = 0;
+  const uint32_t li = (step + 1) & 1, n = min(d.ctl->n_dirty[li], (uint32_t)P.N);
+  for (uint32_t t = tid; t < n; t += nt) {
+    const int p = d.dlist[(size_t)li * P.N + t];
+    if (p >= NA) d.bfs_cand[p - NA] = step;
+    const int r = d.croot[p];
+    if (r < 0 || atomicExch(&d.cx_alive[r - NA], 0u) != 1u) continue;
+    const int b = r - NA, off = d.cx_off[b], sz = d.cx_size[b];
+    for (int i = 0; i < sz; ++i) {
+      const int m = d.members[off + i];
+      d.croot[m] = -1;
+      if (m >= NA) d.bfs_cand[m - NA] = step;
+    }
+  }
+}
+
+// a bond of protein p formed or broke this step (dirty list of step & 1)
+__device__ __forceinline__ void mark_bond_change(const KParams& P, const Dev& d, int p, uint32_t step) {
+  const uint32_t li = step & 1;
+  const uint32_t t = atomicAdd(&d.ctl->n_dirty[li], 1u);
+  if (t < (uint32_t)P.N) d.dlist[(size_t)li * P.N + t] = p;
+  else atomicOr(&d.ctl->err, ERR_MEMBERS);
+}
+
+// ================================================================ BFS
+// Complex of ligand root b: BFS over the bond graph exactly as
+// main.cpp:525-561 (receptor neighbours res_nei[2], [3]; ligand neighbours
+// res_nei[2], [3], [4]; a node is enqueued when first seen).  The root is the
+// lowest-indexed ligand of its component; the BFS of any other ligand of the
+// component finds a lower one among its members and registers nothing.
+#define BFS_QCAP 32
+#define BFS_BATCH 4
+
+// the neighbours in three fixed slots (-1 = none), in BFS order
+__device__ __forceinline__ void nbrs3(const KParams& P, const Dev& d, int x, int* y) {
+  const int NA = P.NA, NB = P.NB;
+  if (x < NA) {
+    const int a = A_NEI2(d, x), b = A_NEI3(d, x);
+    y[0] = a > 0 ? a - 1 : (b > 0 ? b - 1 : -1);
+    y[1] = a > 0 && b > 0 ? b - 1 : -1;
+    y[2] = -1;
+  } else {
+    const int lb = x - NA;
+    const int v2 = B_NEI(d, lb, 2), v3 = B_NEI(d, lb, 3), v4 = B_NEI(d, lb, 4);
+    y[0] = v2 > 0 ? v2 - 1 : -1;
+    y[1] = v3 > 0 ? v3 - 1 : -1;
+    y[2] = v4 > 0 ? v4 - 1 : -1;
+  }
+}
+
 // Complex descriptor (cx_list / cx_heavy): x = root ligand lb | CXD_MOVED
 // (rigid move already done by k_complex), y = members[] offset, z = size |
 // ligands << 16, w = the root's reference index (its random-stream key).
@@ -231,7 +299,7 @@ template <int STRIDE = 1>
 __device__ __forceinline__ void register_complex(const KParams& P, const Dev& d, int p, const int* q, int qn, bool listed) {
   const int NA = P.NA, NB = P.NB;
   uint32_t off = wave_alloc(&d.ctl->cx_cursor, (uint32_t)qn);
-  if (off + qn > (uint32_t)P.N) {  // inconsistent bond graph: the step is undone (kmc_step)
+  if (off + qn > d.mcap) {  // cannot happen below mcap / 2 + N (k_cx_kill): the step is undone (kmc_step)
     atomicOr(&d.ctl->err, ERR_MEMBERS);
     qn = 0;
     off = 0;
@@ -243,8 +311,10 @@ __device__ __forceinline__ void register_complex(const KParams& P, const Dev& d,
     int m = q[t * STRIDE];
     d.members[off + t] = m;
     d.owner[m] = rootid;
+    d.croot[m] = p;
     nb += m >= NA;
   }
+  d.cx_alive[p - NA] = 1;
   const bool staged = listed && qn <= CXL;
   int b = p - NA;
   d.cx_off[b] = (int)off;
@@ -269,6 +339,7 @@ __global__ void __launch_bounds__(256) k_bfs(KParams P, Dev d) {
   const int NA = P.NA, NB = P.NB;
   int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= NB) return;
+  if (!d.ctl->full_now && d.bfs_cand[b] != d.ctl->step) return;  // its complex is kept (k_cx_kill)
   if (B_NEI(d, b, 2) == 0 && B_NEI(d, b, 3) == 0 && B_NEI(d, b, 4) == 0) return;
   int* q = qs + threadIdx.x;  // q[t * 256]
   int p = NA + b;
@@ -775,12 +846,14 @@ struct Stamper {
 // position t in the BFS row, encoded like protein numbers so that the
 // reference's kind tests carry over unchanged: receptor t -> t, ligand t ->
 // NA + t.  Larger complexes (rare) run the same code on global memory.
+#define CX_SHUF 6  // random_shuffle passes whose draws are precomputed (4 + 2 repeats of lable4)
 struct CxLds {
   double bead[CXL][48];  // R_new of member t: receptor bead (j,k) at ((j-1)*4+(k-1))*3+c, ligand ((j-1)*2+(k-1))*3+c
   int lk[CXL][4];        // links (encoded): receptor {nei4 (site), nei2, nei3, -}, ligand {-, nei2, nei3, nei4}
   int slot[CXL];         // slot of member t
   int res[CXL];          // member row (encoded), shuffled in place like results[c][.]
   uint8_t mv[CXL];       // moved flags of this step (main.cpp:122)
+  uint32_t rnd[CX_SHUF][CXL];  // the first CX_SHUF shuffles' keyed draws, computed by all lanes at once
 };
 struct LdsBeads {
   CxLds* L;
@@ -821,6 +894,7 @@ struct CxT {
   S N;              // R_new
   L lk;
   uint32_t* err;
+  const uint32_t (*pre)[CXL] = nullptr;  // precomputed draws of the first CX_SHUF shuffles (LDS), or none
   __device__ int neiA2(int a) const { return lk.a2(a); }
   __device__ int neiA3(int a) const { return lk.a3(a); }
   __device__ int neiA4(int a) const { return lk.a4(a); }
@@ -836,6 +910,7 @@ struct CxT {
   __device__ bool is_moved(int m) const { return lk.moved(m); }
   __device__ void set_moved(int m) const { lk.set_moved(m); }
   __device__ uint32_t shuf_rand(uint32_t call, uint32_t pos) const {
+    if (pre && call < CX_SHUF) return pre[call][pos];
     return kmcr::rand31(P.key, kmcr::DOM_SHUF, rootid, call, step, pos);
   }
   // libstdc++ random_shuffle over res[0 .. size-2] (main.cpp:1285)
@@ -1388,8 +1463,12 @@ __global__ void __launch_bounds__(256) k_complex_heavy(KParams P, Dev d) {
   CxLds* L = &lds[threadIdx.x >> 6];
   const uint32_t step = d.ctl->step;
   auto global_path = [&](int lb) {
-    int* grow = d.members + d.cx_off[lb];
     const int csize = d.cx_size[lb], nB = d.cx_nb[lb];
+    const int* brow = d.members + d.cx_off[lb];  // BFS order (kept across steps)
+    int* grow = d.shuf + d.cx_off[lb];           // the working row the shuffles permute
+    for (int q = lane; q < csize; q += 64) grow[q] = brow[q];
+    if (lane == 0) d.shuf_tag[lb] = step;
+    wave_sync();
     cx_rigid<false>(P, d, L, grow, csize, nB, (uint32_t)d.id_of[NA + lb], step, lane,
                     cx_bead0<false>(P, d, L, grow, csize, lane));
     wave_sync();
@@ -1433,16 +1512,24 @@ __global__ void __launch_bounds__(256) k_complex_heavy(KParams P, Dev d) {
       b[1] = d.nxt.P(m, bj, bk, 1);
       b[2] = d.nxt.P(m, bj, bk, 2);
     }
+    if (nB > 1)  // the shuffles' keyed draws, all at once (main.cpp:1285, 1345, 1413, 1597)
+      for (int e = lane; e < CX_SHUF * CXL; e += 64) {
+        const int call = e / CXL, pos = e % CXL;
+        if (pos >= 1 && pos < csize - 1)
+          L->rnd[call][pos] = kmcr::rand31(P.key, kmcr::DOM_SHUF, (uint32_t)desc.w, call, step, pos);
+      }
     wave_sync();
     if (lane == 0) {
       int pA = -1;  // last receptor in member order
       for (int q = csize - 1; q >= 0 && pA < 0; --q)
         if (L->slot[q] < NA) pA = q;
-      CxT<LdsBeads, LdsLinks> X{P, step, (uint32_t)desc.w, L->res, csize, LdsBeads{L}, LdsLinks{L, NA}, &d.ctl->err};
+      CxT<LdsBeads, LdsLinks> X{P, step, (uint32_t)desc.w, L->res, csize, LdsBeads{L}, LdsLinks{L, NA}, &d.ctl->err,
+                                L->rnd};
       complex_align(X, nB, 0, pA);  // the root is member 0
     }
     wave_sync();
-    cx_write_back(d, L, d.members + desc.y, csize, nB, NA, lane);
+    cx_write_back(d, L, d.shuf + desc.y, csize, nB, NA, lane);  // shuffled row: shuf (members keeps BFS order)
+    if (nB > 1 && lane == 0) d.shuf_tag[lb] = step;
     cx_count(P, d, L, csize, lane, lane < csize ? d.rank[L->slot[lane]].x : 0);  // old rank: k_complex
     wave_sync();
   }
@@ -2502,6 +2589,8 @@ __device__ void rl_match(const KParams& P, const Dev& d) {
     B_NEI(d, lb, k) = i + 1;
     A_NEI2(d, i) = q + 1;
     A_NEI4(d, i) = k;
+    mark_bond_change(P, d, i, d.ctl->step);
+    mark_bond_change(P, d, q, d.ctl->step);
   }
 }
 
@@ -2542,6 +2631,8 @@ __device__ void cis_match(const KParams& P, const Dev& d) {
         A_ST3(d, q) = 1;
         A_NEI3(d, q) = i + 1;
         A_NEI3(d, i) = q + 1;
+        mark_bond_change(P, d, i, d.ctl->step);
+        mark_bond_change(P, d, q, d.ctl->step);
       }
     }
     __syncthreads();
@@ -2562,6 +2653,8 @@ __device__ __forceinline__ bool cis_diss(const KParams& P, const Dev& d, int i, 
     A_ST3(d, q) = 0;
     A_NEI3(d, i) = 0;
     A_NEI3(d, q) = 0;
+    mark_bond_change(P, d, i, step);
+    mark_bond_change(P, d, q, step);
     return true;
   }
   return false;
@@ -2618,6 +2711,8 @@ __global__ void __launch_bounds__(256) k_diss_observe(KParams P, Dev d) {
       A_NEI2(d, i) = 0;
       A_NEI4(d, i) = 0;
       B_NEI(d, lb, k) = 0;
+      mark_bond_change(P, d, i, step);
+      mark_bond_change(P, d, q, step);
       st2_i = 0;
     }
     v[0] = st2_i;
@@ -2716,7 +2811,7 @@ __global__ void __launch_bounds__(256) k_finalize(KParams P, Dev d, double time_
   c->last[6] = n_cisc;
   c->last[7] = n_ovf;
   c->n_overflow = 0;
-  c->cx_cursor = 0;
+  c->n_dirty[(step + 1) & 1] = 0;  // consumed by this step's k_cx_kill; the next step's reactions fill it
   c->n_cx = 0;
   c->n_heavy = 0;
   c->n_pend = 0;
