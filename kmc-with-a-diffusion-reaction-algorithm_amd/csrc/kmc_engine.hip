@@ -35,12 +35,10 @@ struct kmc_sim {
   Dev d;
   int device = 0;
   hipStream_t stream = nullptr;
-  // complexes: 1 = the complex kernels then k_propose_free on the stream,
-  // 2 = the complex kernels on a side stream beside k_propose_free,
-  // 3 = k_propose_free then the complex kernels
+  // complexes: 1 = the complex kernels, then k_propose_free; 4 = the complex
+  // kernels on a side stream beside k_propose_free (launch_step)
   int cx_mode = 1;
   int cx_grid = 0;
-  size_t free_lds = 0;  // debug (KMC_FREE_LDS): dynamic LDS reserved by k_propose_free, to cap its occupancy
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int64_t step_done = 0;
@@ -69,7 +67,7 @@ struct kmc_sim {
   int64_t resort_every = 100, since_resort = 0;
   int key_bits = 1;
   uint64_t *skeys = nullptr, *skeys2 = nullptr;  // (cell << 32) | grouping key
-  bool group_sort = true;  // members of one unit in consecutive slots (KMC_GROUP_SORT=0: cell only)
+  int group_sort = 2;  // 1: members of one unit in consecutive slots; 2: and complexes after the free units; 0: cell only
   int32_t *svals = nullptr, *svals2 = nullptr, *perm = nullptr, *newslot = nullptr;
   int32_t *a_tmp = nullptr, *b_tmp = nullptr, *id_tmp = nullptr;
   void* sort_tmp = nullptr;
@@ -298,6 +296,7 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   d.mcap = (uint32_t)(3 * (size_t)N);
   rc |= dalloc(s, &d.members, d.mcap);
   rc |= dalloc(s, &d.shuf, d.mcap);
+  rc |= dalloc(s, &d.mrec, d.mcap);
   rc |= dalloc(s, &d.shuf_tag, NB);
   rc |= dalloc(s, &d.croot, N);
   rc |= dalloc(s, &d.cx_alive, NB);
@@ -352,31 +351,14 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
     const char* fb = getenv("KMC_FULL_BFS");
     s->always_full = fb && *fb == '1';
     const char* cm = getenv("KMC_CX_MODE");
-    if (cm && *cm) s->cx_mode = std::max(1, std::min(4, atoi(cm)));
+    if (cm && *cm) s->cx_mode = atoi(cm) == 4 ? 4 : 1;
     // k_complex: enough 4-wave workgroups to fill every CU (dynamic dispatch:
     // surplus workgroups find the list empty and exit)
     s->cx_grid = NB > 0 ? std::min(2048, (NB + 15) / 16) : 0;
-    const char* fl = getenv("KMC_FREE_LDS");
-    if (fl && *fl) s->free_lds = (size_t)std::max(0, std::min(160 * 1024, atoi(fl)));
     const char* cg = getenv("KMC_CX_GRID");
     if (cg && *cg) s->cx_grid = std::max(1, atoi(cg));
-    if (s->cx_mode == 2 || s->cx_mode == 4) {
-      // KMC_SIDE_CUS=n: the side stream's kernels on n CUs spread over the
-      // XCDs (CU mask), the rest of the chip left to the main stream's stream
-      const char* sc = getenv("KMC_SIDE_CUS");
-      int ncu = sc && *sc ? atoi(sc) : 0;
-      hipError_t e = hipSuccess;
-      if (ncu > 0 && ncu < prop.multiProcessorCount) {
-        const int tot = prop.multiProcessorCount;
-        std::vector<uint32_t> mask((tot + 31) / 32, 0u);
-        for (int i = 0; i < ncu; ++i) {
-          const int cu = (int)((int64_t)i * tot / ncu);
-          mask[cu / 32] |= 1u << (cu % 32);
-        }
-        e = hipExtStreamCreateWithCUMask(&s->side, (uint32_t)mask.size(), mask.data());
-      } else {
-        e = hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking);
-      }
+    if (s->cx_mode == 4) {
+      const hipError_t e = hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking);
       if (e != hipSuccess || hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming) != hipSuccess ||
           hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming) != hipSuccess) {
         kmc_destroy(s);
@@ -396,9 +378,9 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
     size_t tb = 0;
     int nmax = std::max(NA, NB);
     const char* gs = getenv("KMC_GROUP_SORT");
-    if (gs && *gs) s->group_sort = *gs != '0';
+    if (gs && *gs) s->group_sort = std::max(0, std::min(2, atoi(gs)));
     if (hipcub::DeviceRadixSort::SortPairs(nullptr, tb, s->skeys, s->skeys2, s->svals, s->svals2, nmax, 0,
-                                           32 + s->key_bits, s->stream) != hipSuccess) {
+                                           64, s->stream) != hipSuccess) {
       kmc_destroy(s);
       return KMC_ERR_HIP;
     }
@@ -480,7 +462,7 @@ static int resort(kmc_sim* s) {
   hipStream_t st = s->stream;
   const int NA = K.NA, NB = K.NB, N = K.N, T = 256;
   k_slot_keys<<<(N + T - 1) / T, T, 0, st>>>(K, d, s->skeys, s->svals, s->group_sort);
-  const int b0 = s->group_sort ? 0 : 32, b1 = 32 + s->key_bits;
+  const int b0 = s->group_sort ? 0 : 32, b1 = s->group_sort == 2 ? 64 : 32 + s->key_bits;
   size_t tb = s->sort_tmp_bytes;
   if (NA > 0)
     HIPCHK(s, hipcub::DeviceRadixSort::SortPairs(s->sort_tmp, tb, s->skeys, s->skeys2, s->svals, s->svals2, NA, b0,
@@ -573,6 +555,7 @@ int kmc_set_state(kmc_sim* s, const kmc_state_view* v) {
   if (rc != KMC_OK) return rc;
   // no unit keys yet: the first slot sort groups by cell only
   HIPCHK(s, hipMemsetAsync(d.owner, 0xff, sizeof(int32_t) * (size_t)(NA + NB), s->stream));
+  HIPCHK(s, hipMemsetAsync(d.croot, 0xff, sizeof(int32_t) * (size_t)(NA + NB), s->stream));
   // reference order = identity slots, then the spatial sort
   k_iota<<<(NA + NB + 255) / 256, 256, 0, s->stream>>>(d.id_of, d.slot_of, NA + NB);
   if (NA > 0)
@@ -736,44 +719,30 @@ static int launch_step(kmc_sim* s, bool re_sort) {
     TIMED(KI_CX_KILL, (k_cx_kill<<<std::min(gN, 1024), T, 0, st>>>(K, d, full)));
   }
   TIMED(KI_CLASSIFY, (k_classify<<<gN, T, 0, st>>>(K, d)));
-  if (s->cx_mode == 4 && K.NB > 0) {
-    // the complex chain (BFS, moves, heavy path) on the side stream beside the
-    // free units: k_propose_free reads only k_classify's unit kinds; the two
-    // sides touch disjoint proteins and count records with commutative atomics
-    Bracket b_(s, KI_PROPOSE, st);
-    HIPCHK(s, hipEventRecord(s->ev_fork, st));
-    HIPCHK(s, hipStreamWaitEvent(s->side, s->ev_fork, 0));
-    TIMED_ON(KI_BFS, s->side, (k_bfs<<<gB, T, 0, s->side>>>(K, d)));
-    TIMED_ON(KI_COMPLEX, s->side, (k_complex<<<s->cx_grid, T, 0, s->side>>>(K, d)));
-    TIMED_ON(KI_CX_HEAVY, s->side, (k_complex_heavy<<<256, T, 0, s->side>>>(K, d)));
-    HIPCHK(s, hipEventRecord(s->ev_join, s->side));
-    TIMED(KI_PROPOSE_FREE, (k_propose_free<<<gN, T, s->free_lds, st>>>(K, d)));
-    HIPCHK(s, hipStreamWaitEvent(st, s->ev_join, 0));
-  } else {
-  if (K.NB > 0) {
-    TIMED(KI_BFS, (k_bfs<<<gB, T, 0, st>>>(K, d)));
-  }
-  // complexes (a wave each: rigid move, lay-down / alignment, record
-  // counts) beside the free units' HBM stream (side
-  // stream) or before it; disjoint proteins, commutative record-count atomics
-  hipStream_t cs = s->cx_mode == 2 ? s->side : st;
-  // KI_PROPOSE brackets the whole proposal phase (fork to join): every
-  // protein's R read and R_new written once, the bench's roofline unit
+  // KI_PROPOSE brackets the whole proposal phase: every protein's R read and
+  // R_new written once (the bench's roofline unit).  Complexes: kept or newly
+  // registered (k_bfs), moved a wave each (k_complex), the few whose lay-down
+  // / alignment changes beads finished by k_complex_heavy; the free units one
+  // thread each.  Disjoint proteins; record counts are commutative atomics.
+  // Measured at the C3 steady state: serial (default) 0.724 ms/step; the
+  // complex chain on a side stream beside k_propose_free (KMC_CX_MODE=4) is
+  // no faster — the two compete for the same memory system.
   {
     Bracket b_(s, KI_PROPOSE, st);
-    if (s->cx_mode == 3) TIMED(KI_PROPOSE_FREE, (k_propose_free<<<gN, T, s->free_lds, st>>>(K, d)));
+    hipStream_t cs = st;
+    if (K.NB > 0 && s->cx_mode == 4) {
+      HIPCHK(s, hipEventRecord(s->ev_fork, st));
+      HIPCHK(s, hipStreamWaitEvent(s->side, s->ev_fork, 0));
+      cs = s->side;
+    }
     if (K.NB > 0) {
-      if (s->cx_mode == 2) {
-        HIPCHK(s, hipEventRecord(s->ev_fork, st));
-        HIPCHK(s, hipStreamWaitEvent(s->side, s->ev_fork, 0));
-      }
+      TIMED_ON(KI_BFS, cs, (k_bfs<<<gB, T, 0, cs>>>(K, d)));
       TIMED_ON(KI_COMPLEX, cs, (k_complex<<<s->cx_grid, T, 0, cs>>>(K, d)));
       TIMED_ON(KI_CX_HEAVY, cs, (k_complex_heavy<<<256, T, 0, cs>>>(K, d)));
-      if (s->cx_mode == 2) HIPCHK(s, hipEventRecord(s->ev_join, s->side));
     }
-    if (s->cx_mode != 3) TIMED(KI_PROPOSE_FREE, (k_propose_free<<<gN, T, s->free_lds, st>>>(K, d)));
-    if (K.NB > 0 && s->cx_mode == 2) HIPCHK(s, hipStreamWaitEvent(st, s->ev_join, 0));
-  }
+    if (K.NB > 0 && s->cx_mode == 4) HIPCHK(s, hipEventRecord(s->ev_join, s->side));
+    TIMED(KI_PROPOSE_FREE, (k_propose_free<<<gN, T, 0, st>>>(K, d)));
+    if (K.NB > 0 && s->cx_mode == 4) HIPCHK(s, hipStreamWaitEvent(st, s->ev_join, 0));
   }
   TIMED(KI_SCAN, {
     // single-pass decoupled look-back scan; cell_cnt[ncell] stays 0, so

@@ -55,6 +55,7 @@ struct Dev {
   int32_t* cx_nb;    // [NB] ligands in complex
   int32_t* members;  // [mcap] BFS rows of the registered complexes (kept across steps, BFS order)
   int32_t* shuf;     // [mcap] the rows after this step's multi-ligand shuffles (cluster.log)
+  int4* mrec;        // [mcap] member records of rows of <= CXL members (register_complex)
   uint32_t* shuf_tag;  // [NB] step whose shuffled row of root lb is in shuf
   uint32_t mcap;     // members[] capacity (3N): rows are appended until a full rebuild
   int32_t* croot;    // [N] slot of the root ligand of the protein's registered complex, -1 none
@@ -316,6 +317,45 @@ __device__ __forceinline__ void register_complex(const KParams& P, const Dev& d,
   }
   d.cx_alive[p - NA] = 1;
   const bool staged = listed && qn <= CXL;
+  if (staged) {
+    // member records: slot + links encoded by BFS position (receptor {slot,
+    // nei2, nei3, nei4 (site)}, ligand {slot, nei2, nei3, nei4}; a protein
+    // link to position t is t + 1 for a receptor, NA + t + 1 for a ligand) —
+    // the LDS image the complex kernels load in one coalesced access, every
+    // step the complex is kept
+    auto enc = [&](int v) -> int {
+      if (v <= 0) return 0;
+      for (int t = 0; t < qn; ++t)
+        if (q[t * STRIDE] == v - 1) return (v - 1 < NA ? t : NA + t) + 1;
+      atomicOr(&d.ctl->err, ERR_RESOLVE);  // a link leaving its component
+      return 0;
+    };
+    for (int t0 = 0; t0 < qn; t0 += 4) {  // the links of four members in flight at once
+      int4 r[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int t = t0 + i, m = t < qn ? q[t * STRIDE] : p;
+        r[i].x = m;
+        if (m < NA) {
+          r[i].y = A_NEI2(d, m);
+          r[i].z = A_NEI3(d, m);
+          r[i].w = A_NEI4(d, m);
+        } else {
+          r[i].y = B_NEI(d, m - NA, 2);
+          r[i].z = B_NEI(d, m - NA, 3);
+          r[i].w = B_NEI(d, m - NA, 4);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (t0 + i >= qn) break;
+        r[i].y = enc(r[i].y);
+        r[i].z = enc(r[i].z);
+        if (r[i].x >= NA) r[i].w = enc(r[i].w);
+        d.mrec[off + t0 + i] = r[i];
+      }
+    }
+  }
   int b = p - NA;
   d.cx_off[b] = (int)off;
   d.cx_size[b] = qn;
@@ -1167,51 +1207,25 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-// LDS image of a complex (lanes < csize): member slots from the BFS row, the
-// links of every member encoded by BFS position (a protein link to member t
-// is t + 1 for a receptor, NA + t + 1 for a ligand; receptor {nei4 (site),
-// nei2, nei3}, ligand {-, nei2, nei3, nei4}).  In three steps so that callers
-// can issue their other loads in the same round: slots (then wave_sync), raw
-// links, encoding.
-__device__ __forceinline__ int cx_stage_slots(const Dev& d, CxLds* L, int off, int csize, int NA, int lane) {
-  int m = -1;
-  if (lane < csize) {
-    m = d.members[off + lane];
-    L->slot[lane] = m;
-    L->res[lane] = m < NA ? lane : NA + lane;
-    L->mv[lane] = 0;
-  }
-  return m;
-}
-__device__ __forceinline__ int3 cx_load_links(const Dev& d, int m, int NA) {
-  const int NB = d.cur.NB;
-  if (m < 0) return make_int3(0, 0, 0);
-  if (m < NA) return make_int3(A_NEI4(d, m), A_NEI2(d, m), A_NEI3(d, m));
-  return make_int3(B_NEI(d, m - NA, 2), B_NEI(d, m - NA, 3), B_NEI(d, m - NA, 4));
-}
-__device__ __forceinline__ void cx_encode_links(const Dev& d, CxLds* L, int m, int3 l, int csize, int NA, int lane) {
-  if (lane >= csize) return;
-  auto enc = [&](int v) -> int {  // slot + 1 -> encoded position + 1 (0 stays 0)
-    if (v <= 0) return 0;
-    for (int t = 0; t < csize; ++t)
-      if (L->slot[t] == v - 1) return (v - 1 < NA ? t : NA + t) + 1;
-    atomicOr(&d.ctl->err, ERR_RESOLVE);  // a link leaving its component
-    return 0;
-  };
-  if (m < NA) {
-    L->lk[lane][0] = l.x;
-    L->lk[lane][1] = enc(l.y);
-    L->lk[lane][2] = enc(l.z);
+// LDS image of a complex (lanes < csize) from the member records
+// register_complex stored: slots and links encoded by BFS position (one
+// coalesced 16-byte load per member); returns the lane's member slot or -1
+__device__ __forceinline__ int cx_stage_mrec(const Dev& d, CxLds* L, int off, int csize, int NA, int lane) {
+  if (lane >= csize) return -1;
+  const int4 r = d.mrec[off + lane];
+  L->slot[lane] = r.x;
+  L->res[lane] = r.x < NA ? lane : NA + lane;
+  L->mv[lane] = 0;
+  if (r.x < NA) {
+    L->lk[lane][0] = r.w;
+    L->lk[lane][1] = r.y;
+    L->lk[lane][2] = r.z;
   } else {
-    L->lk[lane][1] = enc(l.x);
-    L->lk[lane][2] = enc(l.y);
-    L->lk[lane][3] = enc(l.z);
+    L->lk[lane][1] = r.y;
+    L->lk[lane][2] = r.z;
+    L->lk[lane][3] = r.w;
   }
-}
-__device__ __forceinline__ void cx_stage_links(const Dev& d, CxLds* L, int off, int csize, int NA, int lane) {
-  const int m = cx_stage_slots(d, L, off, csize, NA, lane);
-  wave_sync();
-  cx_encode_links(d, L, m, cx_load_links(d, m, NA), csize, NA, lane);
+  return r.x;
 }
 
 // R_new rows of every staged member (paired layout, kmc_device.h), and the
@@ -1410,14 +1424,12 @@ __global__ void __launch_bounds__(256) k_complex(KParams P, Dev d) {
     if (c + nw < n) next = d.cx_list[c + nw];  // prefetch the wave's next descriptor
     const int csize = desc.z & 0xffff, nB = desc.z >> 16;
     S(d, 5);
-    const int m = cx_stage_slots(d, L, desc.y, csize, NA, lane);
+    const int m = cx_stage_mrec(d, L, desc.y, csize, NA, lane);
     wave_sync();
-    // one round of independent loads: the lane's pass-0 bead, its member's
-    // links and old reference point (whose record rank is taken right away)
+    // one round of independent loads: the lane's pass-0 bead and its member's
+    // old reference point (whose record rank is taken right away)
     const Bead0 b0 = cx_bead0<true>(P, d, L, nullptr, csize, lane);
-    const int3 lk = cx_load_links(d, m, NA);
     const int rk_old = m >= 0 ? cx_count_old(P, d, m) : 0;
-    cx_encode_links(d, L, m, lk, csize, NA, lane);
     S(d, 0);
     cx_rigid<true>(P, d, L, nullptr, csize, nB, (uint32_t)desc.w, step, lane, b0);
     wave_sync();
@@ -1502,7 +1514,7 @@ __global__ void __launch_bounds__(256) k_complex_heavy(KParams P, Dev d) {
       continue;
     }
     const int csize = desc.z & 0xffff, nB = desc.z >> 16;
-    cx_stage_links(d, L, desc.y, csize, NA, lane);
+    cx_stage_mrec(d, L, desc.y, csize, NA, lane);
     wave_sync();
     for (int e = lane; e < csize * 16; e += 64) {  // the moved beads back into LDS
       const int q = e >> 4, m = L->slot[q], bj = ((e >> 2) & 3) + 1, bk = (e & 3) + 1;
@@ -2840,7 +2852,11 @@ __device__ __forceinline__ uint32_t slot_key(const KParams& P, double x, double 
 // index as the low word, so the members of one unit occupy consecutive slots
 // of their kind: the complex kernels then touch a few cache lines per bead
 // row instead of one per member.
-__global__ void k_slot_keys(KParams P, Dev d, uint64_t* keys, int32_t* vals, bool group) {
+// group 2: members of complexes go after every other protein of their kind
+// (top key bit), so the free units' slots form one dense range: the free
+// proposals then write whole cache lines of R_new, and the complexes' rows
+// are contiguous runs of their own.
+__global__ void k_slot_keys(KParams P, Dev d, uint64_t* keys, int32_t* vals, int group) {
   int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= P.N) return;
   int lead = s, own = d.id_of[s];
@@ -2852,7 +2868,8 @@ __global__ void k_slot_keys(KParams P, Dev d, uint64_t* keys, int32_t* vals, boo
     }
   }
   double x = d.cur.P(lead, 1, 1, 0), y = d.cur.P(lead, 1, 1, 1);
-  keys[s] = (uint64_t)slot_key(P, x, y) << 32 | (uint32_t)(group ? own : 0);
+  const uint64_t tail = group == 2 && d.croot[s] >= 0 ? 1ull << 63 : 0ull;
+  keys[s] = tail | (uint64_t)slot_key(P, x, y) << 32 | (uint32_t)(group ? own : 0);
   vals[s] = s < P.NA ? s : s - P.NA;
 }
 

@@ -18,14 +18,14 @@ timeout -k 10 400 python bench.py --workload $wl --steps 10 --warmup 0 --no-cpu-
 cd /tmp
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run -- \
-  python3 "$root/bench.py" --workload $wl --load-state $state --steps 30 --warmup 5 --no-cpu-baseline \
+  python3 "$root/bench.py" --workload $wl --load-state $state --steps 30 --warmup 105 --no-cpu-baseline \
   > "$out/bench.json" 2> "$out/trace.err"
 python3 "$root/tools/prof_summary.py" "$(find "$out/trace" -name '*kernel_trace.csv' -print -quit)" 5 > "$out/summary.txt"
 python3 "$root/tools/step_timeline.py" "$(find "$out/trace" -name '*kernel_trace.csv' -print -quit)" 3 > "$out/timeline.txt"
 if [ "$pmc" = "pmc" ] || [ "$pmc" = "all" ]; then
   for p in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $p --output-format csv -d "$out/$p" -o run -- \
-      python3 "$root/bench.py" --workload $wl --load-state $state --steps 30 --warmup 5 --no-cpu-baseline \
+      python3 "$root/bench.py" --workload $wl --load-state $state --steps 30 --warmup 105 --no-cpu-baseline \
       > "$out/$p.log" 2>&1
   done
   python3 "$root/tools/pmc_traffic.py" "$(find "$out/FETCH_SIZE" -name '*counter_collection.csv' -print -quit)" \
@@ -36,7 +36,7 @@ if [ "$pmc" = "sq" ] || [ "$pmc" = "all" ]; then
     local name=$1
     shift
     timeout -s KILL 120 rocprofv3 --kernel-trace --pmc "$@" --output-format csv -d "$out/$name" -o run -- \
-      python3 "$root/bench.py" --workload $wl --load-state $state --steps 30 --warmup 5 --no-cpu-baseline \
+      python3 "$root/bench.py" --workload $wl --load-state $state --steps 30 --warmup 105 --no-cpu-baseline \
       > "$out/$name.log" 2>&1
   }
   run_pmc sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES
