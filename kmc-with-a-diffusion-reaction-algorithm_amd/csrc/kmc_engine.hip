@@ -304,7 +304,7 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   rc |= dalloc(s, &d.dlist, 2 * (size_t)N);
   rc |= dalloc(s, &d.pend, N);
   rc |= dalloc(s, &d.overflow, NB);
-  rc |= dalloc(s, &d.cx_list, NB);
+  rc |= dalloc(s, &d.cx_list, (size_t)d.mcap / 2);  // kept across steps: every registration since the last rebuild
   rc |= dalloc(s, &d.cx_heavy, NB);
   rc |= dalloc(s, &d.cell_cnt, s->ncell + 1);
   rc |= dalloc(s, &d.cell_cnt_alt, s->ncell + 1);
@@ -738,7 +738,7 @@ static int launch_step(kmc_sim* s, bool re_sort) {
     if (K.NB > 0) {
       TIMED_ON(KI_BFS, cs, (k_bfs<<<gB, T, 0, cs>>>(K, d)));
       TIMED_ON(KI_COMPLEX, cs, (k_complex<<<s->cx_grid, T, 0, cs>>>(K, d)));
-      TIMED_ON(KI_CX_HEAVY, cs, (k_complex_heavy<<<256, T, 0, cs>>>(K, d)));
+      TIMED_ON(KI_CX_HEAVY, cs, (k_complex_heavy<<<1024, T, 0, cs>>>(K, d)));
     }
     if (K.NB > 0 && s->cx_mode == 4) HIPCHK(s, hipEventRecord(s->ev_join, s->side));
     TIMED(KI_PROPOSE_FREE, (k_propose_free<<<gN, T, 0, st>>>(K, d)));

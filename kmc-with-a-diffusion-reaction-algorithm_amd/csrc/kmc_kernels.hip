@@ -197,18 +197,11 @@ __global__ void k_classify(KParams P, Dev d) {
     }
   }
   // a member of a complex registered in an earlier step and untouched since
-  // (k_cx_kill): its unit is that complex; its root lists it for the complex
-  // kernels (new complexes are registered and listed by k_bfs)
+  // (k_cx_kill): its unit is that complex (new ones are registered by k_bfs)
   const int r = d.croot[p];
   if (r >= 0) {
     own = r;
-    if (r == p) {
-      kind = U_COMPLEX;
-      const int b = p - NA, off = d.cx_off[b], sz = d.cx_size[b], nb = d.cx_nb[b];
-      const int4 desc = make_int4(b, off, sz | nb << 16, d.id_of[p]);
-      if (sz <= CXL) d.cx_list[wave_slot(&d.ctl->n_cx)] = desc;
-      else d.cx_heavy[wave_slot(&d.ctl->n_heavy)] = desc;
-    }
+    if (r == p) kind = U_COMPLEX;
   }
   d.ukind[p] = kind;
   d.owner[p] = own < 0 ? -1 : d.id_of[own];  // -1: member of a complex k_bfs registers this step
@@ -232,6 +225,7 @@ __global__ void k_cx_kill(KParams P, Dev d, int full) {
     for (uint32_t b = tid; b < (uint32_t)P.NB; b += nt) d.cx_alive[b] = 0;
     if (tid == 0) {
       d.ctl->cx_cursor = 0;
+      d.ctl->n_cx = 0;
       d.ctl->full_now = 1;
     }
     return;
@@ -293,11 +287,11 @@ __device__ __forceinline__ void nbrs3(const KParams& P, const Dev& d, int x, int
 #define CXD_LB 0x3fffffff
 
 // Register the component in queue q (q[t * STRIDE], t < qn, BFS order) rooted
-// at ligand slot p: member row, owner keys, descriptor — on cx_list for a
-// complex of at most CXL members (k_complex stages it in LDS), else on the
-// heavy list (global-memory path).
+// at ligand slot p: member row, owner keys, descriptor on cx_list (k_complex
+// stages complexes of at most CXL members in LDS and hands larger ones to the
+// global-memory path of k_complex_heavy).
 template <int STRIDE = 1>
-__device__ __forceinline__ void register_complex(const KParams& P, const Dev& d, int p, const int* q, int qn, bool listed) {
+__device__ __forceinline__ void register_complex(const KParams& P, const Dev& d, int p, const int* q, int qn) {
   const int NA = P.NA, NB = P.NB;
   uint32_t off = wave_alloc(&d.ctl->cx_cursor, (uint32_t)qn);
   if (off + qn > d.mcap) {  // cannot happen below mcap / 2 + N (k_cx_kill): the step is undone (kmc_step)
@@ -316,8 +310,7 @@ __device__ __forceinline__ void register_complex(const KParams& P, const Dev& d,
     nb += m >= NA;
   }
   d.cx_alive[p - NA] = 1;
-  const bool staged = listed && qn <= CXL;
-  if (staged) {
+  if (qn <= CXL) {
     // member records: slot + links encoded by BFS position (receptor {slot,
     // nei2, nei3, nei4 (site)}, ligand {slot, nei2, nei3, nei4}; a protein
     // link to position t is t + 1 for a receptor, NA + t + 1 for a ligand) —
@@ -361,11 +354,12 @@ __device__ __forceinline__ void register_complex(const KParams& P, const Dev& d,
   d.cx_size[b] = qn;
   d.cx_nb[b] = nb;
   d.ukind[p] = U_COMPLEX;
-  if (listed) {
-    const int4 desc = make_int4(b, (int)off, qn | nb << 16, rootid);
-    if (staged) d.cx_list[wave_slot(&d.ctl->n_cx)] = desc;
-    else d.cx_heavy[wave_slot(&d.ctl->n_heavy)] = desc;
-  }
+  // the descriptor list is kept across steps too: a descriptor is current
+  // while its root is alive with the same row offset (k_complex checks)
+  const int4 desc = make_int4(b, (int)off, qn | nb << 16, rootid);
+  const uint32_t slot = wave_slot(&d.ctl->n_cx);
+  if (slot < d.mcap / 2) d.cx_list[slot] = desc;
+  else atomicOr(&d.ctl->err, ERR_MEMBERS);
 }
 
 // One thread per bonded ligand; the queue lives in LDS, one column per thread
@@ -437,7 +431,7 @@ __global__ void __launch_bounds__(256) k_bfs(KParams P, Dev d) {
     head += nb;
   }
   if (lower(qn)) return;
-  register_complex<256>(P, d, p, q, qn, true);
+  register_complex<256>(P, d, p, q, qn);
 }
 
 // Component of overflow entry o (larger than BFS_QCAP): one thread, global
@@ -466,7 +460,7 @@ __device__ __forceinline__ int bfs_overflow_one(const KParams& P, const Dev& d, 
       q[qn++] = v;
     }
   }
-  register_complex(P, d, p, q, qn, false);
+  register_complex(P, d, p, q, qn);
   return p - NA;
 }
 
@@ -1423,6 +1417,13 @@ __global__ void __launch_bounds__(256) k_complex(KParams P, Dev d) {
     const int4 desc = next;
     if (c + nw < n) next = d.cx_list[c + nw];  // prefetch the wave's next descriptor
     const int csize = desc.z & 0xffff, nB = desc.z >> 16;
+    // a descriptor of a dissolved complex (k_cx_kill), or of an older row of a
+    // root registered anew, is skipped
+    if (d.cx_alive[desc.x] != 1u || d.cx_off[desc.x] != desc.y) continue;
+    if (csize > CXL) {  // the global-memory path: rigid move and alignment in k_complex_heavy
+      if (lane == 0) d.cx_heavy[atomicAdd(&d.ctl->n_heavy, 1u)] = desc;
+      continue;
+    }
     S(d, 5);
     const int m = cx_stage_mrec(d, L, desc.y, csize, NA, lane);
     wave_sync();
@@ -2824,7 +2825,6 @@ __global__ void __launch_bounds__(256) k_finalize(KParams P, Dev d, double time_
   c->last[7] = n_ovf;
   c->n_overflow = 0;
   c->n_dirty[(step + 1) & 1] = 0;  // consumed by this step's k_cx_kill; the next step's reactions fill it
-  c->n_cx = 0;
   c->n_heavy = 0;
   c->n_pend = 0;
   c->n_rl = 0;
