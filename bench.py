@@ -55,8 +55,9 @@ def kernel_bytes(name: str, n_a: int, n_b: int):
     """Algorithmic HBM bytes per launch."""
     n = n_a + n_b
     models = {
-        # read R (16 receptor / 8 ligand beads × xyz × 8 B), write R_new, unit
-        # kind; the record counts it also takes write one rank pair per protein
+        # the proposal phase (PROPOSE_PHASE): every protein's R read (16
+        # receptor / 8 ligand beads × xyz × 8 B) and R_new written, its unit
+        # kind read, its record ranks written
         "k_propose": 768 * n_a + 384 * n_b + n + 8 * n,
         # every record once (float4 + id)
         "k_col_scan": 2 * n * 24,
@@ -75,15 +76,24 @@ def kernel_bytes(name: str, n_a: int, n_b: int):
 TRAFFIC_JSON = "profiles/traffic_C3.json"
 
 
+# the proposal phase the engine brackets as "k_propose" (kmc_engine.hip
+# launch_step): these kernels back to back on the engine's stream
+PROPOSE_PHASE = ("k_bfs", "k_complex", "k_complex_heavy", "k_propose_free")
+
+
 def pmc_traffic(kernel: str, workload: str):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
-    (FETCH_SIZE + WRITE_SIZE, tools/pmc_traffic.py) of this same bench
-    command; None when no profile of this workload is committed."""
+    """HBM bytes per launch of `kernel` (the proposal phase: the sum over its
+    kernels) from the committed rocprofv3 PMC passes (FETCH_SIZE + WRITE_SIZE,
+    tools/pmc_traffic.py) of this same bench at the steady state
+    (tools/gpu_steady_profile.sh); None when no profile of this workload is
+    committed."""
     path = os.path.join(REPO, TRAFFIC_JSON)
     if workload != "C3" or not os.path.exists(path):
         return None
-    rec = json.load(open(path)).get(kernel_trace_name(kernel))
-    return rec["traffic_bytes"] if rec else None
+    t = json.load(open(path))
+    names = PROPOSE_PHASE if kernel == "k_propose" else (kernel_trace_name(kernel),)
+    recs = [t.get(n) for n in names]
+    return sum(r["traffic_bytes"] for r in recs) if all(recs) else None
 
 
 def kernel_trace_name(name: str) -> str:
@@ -341,6 +351,7 @@ def run_rank(args, rank: int, world: int, local: int):
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                 "traffic": traffic,
                 "traffic_source": TRAFFIC_JSON if traffic is not None else None,
+                "kernels": list(PROPOSE_PHASE) if dom == "k_propose" else [kernel_trace_name(dom)],
                 "bytes_per_launch": kb,
                 "avg_launch_ms": avg_s * 1e3,
                 "step_bytes": step_b,
