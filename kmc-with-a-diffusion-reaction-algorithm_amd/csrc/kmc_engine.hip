@@ -19,12 +19,14 @@ using namespace kmcd;
 
 // kernel ids for per-kernel HIP-event timing (kmc_set_timing / kmc_kernel_times)
 enum KId {
-  KI_CLASSIFY, KI_BFS, KI_PROPOSE, KI_PROPOSE_FREE, KI_COMPLEX, KI_CX_HEAVY, KI_CX_KILL, KI_SCAN, KI_REC_SCATTER,
+  KI_CLASSIFY, KI_BFS, KI_PROPOSE, KI_PROPOSE_FREE, KI_MOVE_MEMBERS, KI_COMPLEX, KI_CX_CHECK, KI_CX_HEAVY, KI_CX_KILL, KI_SCAN,
+  KI_REC_SCATTER,
   KI_COL_SCAN, KI_COL_EXACT, KI_COL_ROUNDS, KI_COMMIT, KI_RXN_SCAN, KI_RXN_EXACT, KI_MATCH, KI_DISS_OBSERVE,
   KI_RESORT, KI_N
 };
 static const char* const KNAMES[KI_N] = {
-    "k_classify", "k_bfs", "k_propose", "k_propose_free", "k_complex", "k_complex_heavy", "k_cx_kill", "k_scan",
+    "k_classify", "k_bfs", "k_propose", "k_propose_free", "k_move_members", "k_cx_params", "k_cx_check", "k_complex_heavy",
+    "k_cx_kill", "k_scan",
     "k_rec_scatter", "k_col_scan", "k_col_exact", "k_col_rounds", "k_commit", "k_rxn_scan", "k_rxn_exact",
     "k_match", "k_diss_observe", "slot_resort"};
 #define TRING 64  // steps of event pairs kept in flight
@@ -35,12 +37,6 @@ struct kmc_sim {
   Dev d;
   int device = 0;
   hipStream_t stream = nullptr;
-  // complexes: 1 = the complex kernels, then k_propose_free; 4 = the complex
-  // kernels on a side stream beside k_propose_free (launch_step)
-  int cx_mode = 1;
-  int cx_grid = 0;
-  hipStream_t side = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int64_t step_done = 0;
   std::string err;
   int ncell = 0;
@@ -297,6 +293,7 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   rc |= dalloc(s, &d.members, d.mcap);
   rc |= dalloc(s, &d.shuf, d.mcap);
   rc |= dalloc(s, &d.mrec, d.mcap);
+  rc |= dalloc(s, &d.cxp, (size_t)NB * CXP);
   rc |= dalloc(s, &d.shuf_tag, NB);
   rc |= dalloc(s, &d.croot, N);
   rc |= dalloc(s, &d.cx_alive, NB);
@@ -347,24 +344,8 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
     const char* te = getenv("KMC_TILE");
     if (te && *te) t = std::max(2, std::min(TILE_MAX, atoi(te)));
     K.tile = t;
-    // k_complex waves: up to one per 4 ligands, at most 4096
     const char* fb = getenv("KMC_FULL_BFS");
     s->always_full = fb && *fb == '1';
-    const char* cm = getenv("KMC_CX_MODE");
-    if (cm && *cm) s->cx_mode = atoi(cm) == 4 ? 4 : 1;
-    // k_complex: enough 4-wave workgroups to fill every CU (dynamic dispatch:
-    // surplus workgroups find the list empty and exit)
-    s->cx_grid = NB > 0 ? std::min(2048, (NB + 15) / 16) : 0;
-    const char* cg = getenv("KMC_CX_GRID");
-    if (cg && *cg) s->cx_grid = std::max(1, atoi(cg));
-    if (s->cx_mode == 4) {
-      const hipError_t e = hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking);
-      if (e != hipSuccess || hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming) != hipSuccess) {
-        kmc_destroy(s);
-        return KMC_ERR_HIP;
-      }
-    }
     const char* ds = getenv("KMC_DEBUG_SCAN_STAGE");
     K.dbg_stage = ds && *ds ? atoi(ds) : 0;
   }
@@ -413,10 +394,6 @@ int kmc_destroy(kmc_sim* s) {
   if (s->ctl_host) (void)hipHostFree(s->ctl_host);
   for (auto& e : s->tev)
     if (e) (void)hipEventDestroy(e);
-  if (s->side) (void)hipStreamSynchronize(s->side);
-  if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);
-  if (s->ev_join) (void)hipEventDestroy(s->ev_join);
-  if (s->side) (void)hipStreamDestroy(s->side);
   if (s->stream) (void)hipStreamDestroy(s->stream);
   delete s;
   return KMC_OK;
@@ -720,29 +697,26 @@ static int launch_step(kmc_sim* s, bool re_sort) {
   }
   TIMED(KI_CLASSIFY, (k_classify<<<gN, T, 0, st>>>(K, d)));
   // KI_PROPOSE brackets the whole proposal phase: every protein's R read and
-  // R_new written once (the bench's roofline unit).  Complexes: kept or newly
-  // registered (k_bfs), moved a wave each (k_complex), the few whose lay-down
-  // / alignment changes beads finished by k_complex_heavy; the free units one
-  // thread each.  Disjoint proteins; record counts are commutative atomics.
-  // Measured at the C3 steady state: serial (default) 0.724 ms/step; the
-  // complex chain on a side stream beside k_propose_free (KMC_CX_MODE=4) is
-  // no faster — the two compete for the same memory system.
+  // R_new written once (the bench's roofline unit).  Complexes kept or newly
+  // registered (k_bfs); their rigid-move parameters (k_cx_params); every unit
+  // moved by coalesced thread-per-slot streams: free receptors, cis dimers,
+  // free ligands (k_propose_free), members of complexes of <= CXL proteins
+  // (k_move_members, with their complex's parameters); the complexes' lay-down / alignment tests and new
+  // records (k_cx_check); the few complexes whose tests fail, with several
+  // ligands or many members (k_complex_heavy).
   {
     Bracket b_(s, KI_PROPOSE, st);
-    hipStream_t cs = st;
-    if (K.NB > 0 && s->cx_mode == 4) {
-      HIPCHK(s, hipEventRecord(s->ev_fork, st));
-      HIPCHK(s, hipStreamWaitEvent(s->side, s->ev_fork, 0));
-      cs = s->side;
-    }
+    const int gL = std::min(2048, (K.NB + T - 1) / T);  // grid-stride over the descriptor list
     if (K.NB > 0) {
-      TIMED_ON(KI_BFS, cs, (k_bfs<<<gB, T, 0, cs>>>(K, d)));
-      TIMED_ON(KI_COMPLEX, cs, (k_complex<<<s->cx_grid, T, 0, cs>>>(K, d)));
-      TIMED_ON(KI_CX_HEAVY, cs, (k_complex_heavy<<<1024, T, 0, cs>>>(K, d)));
+      TIMED(KI_BFS, (k_bfs<<<gB, T, 0, st>>>(K, d)));
+      TIMED(KI_COMPLEX, (k_cx_params<<<gL, T, 0, st>>>(K, d)));
     }
-    if (K.NB > 0 && s->cx_mode == 4) HIPCHK(s, hipEventRecord(s->ev_join, s->side));
     TIMED(KI_PROPOSE_FREE, (k_propose_free<<<gN, T, 0, st>>>(K, d)));
-    if (K.NB > 0 && s->cx_mode == 4) HIPCHK(s, hipStreamWaitEvent(st, s->ev_join, 0));
+    if (K.NB > 0) {
+      TIMED(KI_MOVE_MEMBERS, (k_move_members<<<gN, T, 0, st>>>(K, d)));
+      TIMED(KI_CX_CHECK, (k_cx_check<<<gL, T, 0, st>>>(K, d)));
+      TIMED(KI_CX_HEAVY, (k_complex_heavy<<<1024, T, 0, st>>>(K, d)));
+    }
   }
   TIMED(KI_SCAN, {
     // single-pass decoupled look-back scan; cell_cnt[ncell] stays 0, so

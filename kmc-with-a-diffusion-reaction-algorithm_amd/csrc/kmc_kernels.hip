@@ -56,6 +56,7 @@ struct Dev {
   int32_t* members;  // [mcap] BFS rows of the registered complexes (kept across steps, BFS order)
   int32_t* shuf;     // [mcap] the rows after this step's multi-ligand shuffles (cluster.log)
   int4* mrec;        // [mcap] member records of rows of <= CXL members (register_complex)
+  double* cxp;       // [NB][16] rigid-move parameters of the complex rooted at lb (k_cx_params)
   uint32_t* shuf_tag;  // [NB] step whose shuffled row of root lb is in shuf
   uint32_t mcap;     // members[] capacity (3N): rows are appended until a full rebuild
   int32_t* croot;    // [N] slot of the root ligand of the protein's registered complex, -1 none
@@ -819,25 +820,6 @@ __device__ void propose_free_b(const KParams& P, const Dev& d, int lb, int p, ui
   count_new(P, d, p, rk_old, scx[0], scy[0], ext);
 }
 
-// One thread per slot: free receptors, cis dimers and free ligands (the
-// complexes were moved by k_complex just before).
-__device__ __forceinline__ void propose_one(const KParams& P, const Dev& d, int p) {
-  if (p >= P.N) return;
-  const uint32_t step = d.ctl->step;
-  const int NA = P.NA;
-  uint8_t k = d.ukind[p];
-  if (k == U_FREE_A) {
-    propose_free_a(P, d, p, step);
-  } else if (k == U_DIMER) {
-    const int q = A_NEI3(d, p) - 1;
-    propose_dimer(P, d, p, q, step);
-    count_records(P, d, p);
-    count_records(P, d, q);
-  } else if (k == U_FREE_B) {
-    propose_free_b(P, d, p - P.NA, p, step);
-  }
-}
-
 // ---------------------------------------------------------------- stamps
 // Diagnostic build only (-DKMC_STAMPS): thread 0 of each workgroup adds the
 // cycles since its previous stamp to ctl->stamps[base + i] (phase shares of
@@ -1394,77 +1376,187 @@ __device__ __forceinline__ void cx_rigid(const KParams& P, const Dev& d, CxLds* 
   }
 }
 
-// k_complex: one wave per complex of up to CXL members, grid-stride over
-// cx_list (a shared dispatch counter would serialise one atomic per complex).
-// The member records and the moved beads live in LDS.  The lay-down /
-// alignment code (main.cpp:1138-1732) changes nothing when every one of its
-// tests passes — a single ligand already laid down (1141), its receptors on
-// their sites (1215) and their cis partners on theirs (1255); these tests are
-// independent when nothing moves, so lanes 0-3 evaluate them in parallel.
-// A complex that passes is written back and its records counted here; any
-// other (a test fails, or several ligands: the shuffled multi-ligand passes)
-// is written back as moved and handed to k_complex_heavy, so the register-
-// heavy sequential code stays out of this kernel (occupancy).
-__global__ void __launch_bounds__(256) k_complex(KParams P, Dev d) {
-  __shared__ CxLds lds[4];
-  const int lane = __lane_id(), NA = P.NA;
-  CxLds* L = &lds[threadIdx.x >> 6];
+// ---------------------------------------------------------------- complexes, streamed
+// The rigid move of a complex of at most CXL members (main.cpp:974-1131) in
+// three steps, so that its members' beads are moved by the same coalesced,
+// one-thread-per-slot stream as the free units:
+//   k_cx_params    one thread per complex: the keyed draws, the periodic shift
+//                  and the centre of mass (sums over the members' [1][1] and
+//                  [j][1] beads in BFS member order, 994-1067), the rotation
+//                  matrix -> cxp[root] (16 doubles)
+//   k_propose_units  (a member's thread) every bead moved with its complex's
+//                  parameters — the same expressions as the wave version
+//   k_cx_check     one thread per complex: the lay-down / alignment tests
+//                  (1141, 1215, 1255) on R_new; a complex that passes has its
+//                  members' new records counted, any other (a test fails, or
+//                  several ligands) goes to k_complex_heavy as moved.
+#define CXP 16  // doubles per complex: dx dy PBx PBy cmx cmy cmz t[3][3]
+
+// descriptor c of cx_list: current (root alive with this row) and small
+__device__ __forceinline__ bool cx_current(const Dev& d, int4 desc) {
+  return d.cx_alive[desc.x] == 1u && d.cx_off[desc.x] == desc.y;
+}
+
+__global__ void __launch_bounds__(256) k_cx_params(KParams P, Dev d) {
   const uint32_t n = d.ctl->n_cx, step = d.ctl->step;
-  const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
-  Stamper S(16);
-  int4 next = w < n ? d.cx_list[w] : make_int4(0, 0, 0, 0);
-  for (uint32_t c = w; c < n; c += nw) {
-    const int4 desc = next;
-    if (c + nw < n) next = d.cx_list[c + nw];  // prefetch the wave's next descriptor
-    const int csize = desc.z & 0xffff, nB = desc.z >> 16;
-    // a descriptor of a dissolved complex (k_cx_kill), or of an older row of a
-    // root registered anew, is skipped
-    if (d.cx_alive[desc.x] != 1u || d.cx_off[desc.x] != desc.y) continue;
+  for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x) {
+    const int4 desc = d.cx_list[c];
+    if (!cx_current(d, desc)) continue;
+    const int csize = desc.z & 0xffff, nB = desc.z >> 16, nA = csize - nB;
     if (csize > CXL) {  // the global-memory path: rigid move and alignment in k_complex_heavy
-      if (lane == 0) d.cx_heavy[atomicAdd(&d.ctl->n_heavy, 1u)] = desc;
+      d.cx_heavy[atomicAdd(&d.ctl->n_heavy, 1u)] = desc;
       continue;
     }
-    S(d, 5);
-    const int m = cx_stage_mrec(d, L, desc.y, csize, NA, lane);
-    wave_sync();
-    // one round of independent loads: the lane's pass-0 bead and its member's
-    // old reference point (whose record rank is taken right away)
-    const Bead0 b0 = cx_bead0<true>(P, d, L, nullptr, csize, lane);
-    const int rk_old = m >= 0 ? cx_count_old(P, d, m) : 0;
-    S(d, 0);
-    cx_rigid<true>(P, d, L, nullptr, csize, nB, (uint32_t)desc.w, step, lane, b0);
-    wave_sync();
-    S(d, 1);
-    bool bad = false;
-    if (nB == 1 && lane < 4) {  // the root is member 0, the complex's only ligand
-      const LdsBeads N{L};
-      if (lane == 0) {
-        bad = N.B(0, 1, 2, 2) != (N.B(0, 1, 1, 2) + P.rb);
-      } else {
-        const int j = lane + 1, a1ref = L->lk[0][j - 1];
-        if (a1ref != 0) {
-          const int a1 = a1ref - 1, a2ref = L->lk[a1][2];
-          bad = bond_misaligned(P, N, 0, j, a1) || (a2ref != 0 && cis_misaligned(P, N, a1, a2ref - 1));
+    double u0, u1, u2, u3;
+    kmcr::uniform2(P.key, kmcr::DOM_DIFF, (uint32_t)desc.w, 0, step, 0, &u0, &u1);
+    kmcr::uniform2(P.key, kmcr::DOM_DIFF, (uint32_t)desc.w, 0, step, 1, &u2, &u3);
+    double amp = (nB == 1 ? P.amp_bond : 0.0) * u0;
+    double phai = u1 * 2 * P.pai;
+    double dx = amp * kmcm::cos(phai), dy = amp * kmcm::sin(phai);
+    const int* row = d.members + desc.y;
+    // [j][1] beads of four members at a time in registers, summed in member order
+    double PBx = 0, PBy = 0, cmx = 0, cmy = 0, cmz = 0;
+    for (int pass = 0; pass < 2; ++pass) {
+      for (int t0 = 0; t0 < csize; t0 += 4) {
+        double2 xy[4][4];
+        double z[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int t = t0 + i;
+          if (t >= csize) break;
+          const int m = row[t];
+          if (pass == 0) {
+            xy[i][0] = m < P.NA ? d.cur.Axy(m, 1, 1) : d.cur.Bxy(m - P.NA, 1, 1);
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              xy[i][j] = m < P.NA ? d.cur.Axy(m, j + 1, 1) : d.cur.Bxy(m - P.NA, j + 1, 1);
+              z[i][j] = d.cur.P(m, j + 1, 1, 2);
+            }
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (t0 + i >= csize) break;
+          if (pass == 0) {
+            PBx = PBx + (xy[i][0].x + dx);
+            PBy = PBy + (xy[i][0].y + dy);
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              cmx = cmx + ((xy[i][j].x + dx) - PBx);
+              cmy = cmy + ((xy[i][j].y + dy) - PBy);
+              cmz = cmz + z[i][j];
+            }
+          }
         }
       }
+      if (pass == 0) {
+        PBx = P.box_x * kmcm::round_(PBx / (nA + nB) / P.box_x);
+        PBy = P.box_y * kmcm::round_(PBy / (nA + nB) / P.box_y);
+      }
     }
-    const bool heavy = nB != 1 || __ballot(bad) != 0;
-    S(d, 2);
-    cx_write_back(d, L, nullptr, csize, 1, NA, lane);
-    S(d, 3);
-    if (heavy) {
-      // k_complex_heavy counts the new records; the old ranks are kept
-      if (lane < csize) d.rank[m] = make_int2(rk_old, -1);
-      if (lane == 0) d.cx_heavy[atomicAdd(&d.ctl->n_heavy, 1u)] = make_int4(desc.x | CXD_MOVED, desc.y, desc.z, desc.w);
-    } else {
-      cx_count(P, d, L, csize, lane, rk_old);
-    }
-    wave_sync();
-    S(d, 4);
+    cmx = cmx / (4 * nA + 4 * nB);
+    cmy = cmy / (4 * nA + 4 * nB);
+    cmz = cmz / (4 * nA + 4 * nB);
+    const Rot t = euler(0, 0, (2 * u2 - 1) * (nB == 1 ? P.rot_bond : 0.0));
+    double* o = d.cxp + (size_t)desc.x * CXP;
+    o[0] = dx;
+    o[1] = dy;
+    o[2] = PBx;
+    o[3] = PBy;
+    o[4] = cmx;
+    o[5] = cmy;
+    o[6] = cmz;
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+      for (int b = 0; b < 3; ++b) o[7 + a * 3 + b] = t.t[a][b];
   }
 }
 
-// k_complex_heavy: the complexes k_complex did not finish.  Staged ones (<=
+// member i (receptor: IS_A, or ligand) of a streamed complex: all beads moved
+// with the complex's parameters (every coordinate loaded first, as the free
+// units; compile-time row indices keep them in registers); the old record is
+// counted here, the new one by k_cx_check / k_complex_heavy
+template <bool IS_A>
+__device__ __forceinline__ void move_member(const KParams& P, const Dev& d, int i, const double* cp) {
+  constexpr int NK = IS_A ? 4 : 2, ROWS = IS_A ? ROWS_A : ROWS_B;
+  const int n = IS_A ? P.NA : P.NB, p = IS_A ? i : P.NA + i;
+  const double2* src = reinterpret_cast<const double2*>(IS_A ? d.cur.a : d.cur.b);
+  double2* dst = reinterpret_cast<double2*>(IS_A ? d.nxt.a : d.nxt.b);
+  double2 r[ROWS];
+#pragma unroll
+  for (int w = 0; w < ROWS; ++w) r[w] = ld_r(src[(size_t)w * n + i]);
+  const double dx = cp[0], dy = cp[1], PBx = cp[2], PBy = cp[3], cmx = cp[4], cmy = cp[5], cmz = cp[6];
+  Rot t;
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int b = 0; b < 3; ++b) t.t[a][b] = cp[7 + a * 3 + b];
+  d.rank[p].x = atomicAdd(&d.cell_cnt[rec_cell(P, r[0].x, r[0].y, IS_A ? 0 : 1)], 1);
+  // beads (j, k) and (j+1, k), j odd: xy rows (j-1)·NK + (k-1) and j·NK + (k-1),
+  // their z pair in row 4·NK + ((j-1)>>1)·NK + (k-1); moved in place
+#pragma unroll
+  for (int jp = 0; jp < 2; ++jp)
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const int r1 = 2 * jp * NK + k, r2 = (2 * jp + 1) * NK + k, rzr = 4 * NK + jp * NK + k;
+      const double z1 = r[rzr].x, z2 = r[rzr].y;
+      const double ox1 = (r[r1].x + dx) - PBx, oy1 = (r[r1].y + dy) - PBy;
+      const double ox2 = (r[r2].x + dx) - PBx, oy2 = (r[r2].y + dy) - PBy;
+      r[r1] = make_double2(rx(t, ox1, oy1, z1, cmx, cmy, cmz), ry(t, ox1, oy1, z1, cmx, cmy, cmz));
+      r[r2] = make_double2(rx(t, ox2, oy2, z2, cmx, cmy, cmz), ry(t, ox2, oy2, z2, cmx, cmy, cmz));
+      r[rzr] = make_double2(rz(t, ox1, oy1, z1, cmx, cmy, cmz), rz(t, ox2, oy2, z2, cmx, cmy, cmz));
+    }
+#pragma unroll
+  for (int w = 0; w < ROWS; ++w) st_n(dst[(size_t)w * n + i], r[w]);
+}
+
+__global__ void __launch_bounds__(256) k_cx_check(KParams P, Dev d) {
+  const int NA = P.NA, NB = P.NB;
+  const uint32_t n = d.ctl->n_cx;
+  const Beads& N = d.nxt;
+  for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x) {
+    const int4 desc = d.cx_list[c];
+    if (!cx_current(d, desc)) continue;
+    const int csize = desc.z & 0xffff, nB = desc.z >> 16;
+    if (csize > CXL) continue;
+    bool heavy = nB != 1;
+    if (!heavy) {
+      const int lb = desc.x;  // the root: the complex's only ligand
+      heavy = N.B(lb, 1, 2, 2) != (N.B(lb, 1, 1, 2) + P.rb);
+#pragma unroll
+      for (int j = 2; j <= 4; ++j) {
+        const int a1ref = B_NEI(d, lb, j);
+        if (a1ref == 0) continue;
+        const int a1 = a1ref - 1, a2ref = A_NEI3(d, a1);
+        heavy |= bond_misaligned(P, N, lb, j, a1) || (a2ref != 0 && cis_misaligned(P, N, a1, a2ref - 1));
+      }
+    }
+    if (heavy) {
+      d.cx_heavy[atomicAdd(&d.ctl->n_heavy, 1u)] = make_int4(desc.x | CXD_MOVED, desc.y, desc.z, desc.w);
+      continue;
+    }
+    const int* row = d.members + desc.y;
+    for (int t = 0; t < csize; ++t) {  // the members' new records
+      const int m = row[t];
+      const bool isA = m < NA;
+      double2 b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = isA ? N.Axy(m, j + 1, 1) : N.Bxy(m - NA, j + 1, 1);
+      bool ext = true;
+#pragma unroll
+      for (int j = 1; j < 4; ++j) {
+        const double ex = b[j].x - b[0].x, ey = b[j].y - b[0].y;
+        ext &= isA ? ex * ex + ey * ey <= 0.09 : ex * ex + ey * ey <= 35.0 * 35.0;
+      }
+      count_new(P, d, m, d.rank[m].x, b[0].x, b[0].y, ext);
+    }
+  }
+}
+
+// k_complex_heavy: the complexes the streamed path did not finish.  Staged ones (<=
 // CXL members, already moved) are reloaded from R_new into LDS and lane 0
 // runs the lay-down / alignment code against LDS; larger ones run the rigid
 // move and the alignment on global memory.  Block 0's first wave first runs
@@ -1548,7 +1640,37 @@ __global__ void __launch_bounds__(256) k_complex_heavy(KParams P, Dev d) {
   }
 }
 
-// free units (free receptors, cis dimers, free ligands), one thread per slot
+// One thread per slot: free receptors, cis dimers, free ligands.
+__device__ __forceinline__ void propose_one(const KParams& P, const Dev& d, int p) {
+  if (p >= P.N) return;
+  const uint32_t step = d.ctl->step;
+  const int NA = P.NA;
+  uint8_t k = d.ukind[p];
+  if (k == U_FREE_A) {
+    propose_free_a(P, d, p, step);
+  } else if (k == U_DIMER) {
+    const int q = A_NEI3(d, p) - 1;
+    propose_dimer(P, d, p, q, step);
+    count_records(P, d, p);
+    count_records(P, d, q);
+  } else if (k == U_FREE_B) {
+    propose_free_b(P, d, p - P.NA, p, step);
+  }
+}
+
+// member p of a complex of at most CXL members (k_cx_params), one thread per
+// slot: a separate launch keeps the free units' kernel at 4 waves/SIMD
+__global__ void __launch_bounds__(256) k_move_members(KParams P, Dev d) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x, NA = P.NA;
+  if (p >= P.N) return;
+  const int r = d.croot[p];
+  if (r < 0 || d.cx_size[r - NA] > CXL) return;
+  const double* cp = d.cxp + (size_t)(r - NA) * CXP;
+  if (p < NA) move_member<true>(P, d, p, cp);
+  else move_member<false>(P, d, p - NA, cp);
+}
+
+// the free units, one thread per slot
 __global__ void __launch_bounds__(256) k_propose_free(KParams P, Dev d) {
   propose_one(P, d, (int)(blockIdx.x * blockDim.x + threadIdx.x));
 }
