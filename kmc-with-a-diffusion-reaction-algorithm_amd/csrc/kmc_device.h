@@ -43,6 +43,7 @@ struct Ctl {
   uint32_t n_overflow;    // ligands whose BFS overflowed the register queue
   uint32_t cx_cursor;     // members[] allocation cursor (rows are kept across steps; k_cx_kill resets)
   uint32_t n_pend;        // units still pending after a round (pass C)
+  uint32_t n_pqu, n_pqe;  // compacted pending units / conflict entries for k_col_tail
   uint32_t n_cx;          // complexes registered by the BFS this step (cx_list)
   uint32_t n_heavy;       // entries of cx_heavy this step
   uint32_t full_now;      // k_cx_kill: no complex kept this step (every bonded ligand runs the BFS)

@@ -145,6 +145,7 @@ int alloc_lists(kmc_sim* s) {
   dfree(s, d.cis_keys);
   dfree(s, d.ent);
   dfree(s, d.gi32);
+  dfree(s, d.pq_ent);
   uint32_t cap = (uint32_t)scale(pow2(std::max<uint32_t>(4096, std::min<uint32_t>(1u << 20, (uint32_t)N / 8 + 1))));
   d.cap_edges = pow2(cap);
   int rc = KMC_OK;
@@ -164,6 +165,7 @@ int alloc_lists(kmc_sim* s) {
   rc |= dalloc(s, &d.cis_keys, d.cap_edges);
   rc |= dalloc(s, &d.ent, (size_t)2 * d.cap_edges);
   rc |= dalloc(s, &d.gi32, (size_t)6 * d.cap_edges);
+  rc |= dalloc(s, &d.pq_ent, (size_t)d.conf.cap * NSHARD);
   return rc;
 }
 
@@ -315,6 +317,7 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   }
   rc |= alloc_lists(s);
   rc |= dalloc(s, &d.rank, N);
+  rc |= dalloc(s, &d.pq_units, N);
   rc |= dalloc(s, &d.obs_part, (size_t)8 * ((N + 255) / 256));
   rc |= dalloc(s, &d.bfs_queue, N);
   rc |= dalloc(s, &d.vtag, N);
@@ -732,6 +735,7 @@ static int launch_step(kmc_sim* s, bool re_sort) {
   TIMED(KI_COL_ROUNDS, {
     k_col_round<<<gX, T, 0, st>>>(K, d, 0);
     k_col_units<<<gX, T, 0, st>>>(K, d, 0);
+    k_col_compact<<<gX, T, 0, st>>>(K, d);
     k_col_tail<<<1, 1024, 0, st>>>(K, d, 1);
   });
   TIMED(KI_COMMIT, (k_rej_commit<<<gX, T, 0, st>>>(K, d)));

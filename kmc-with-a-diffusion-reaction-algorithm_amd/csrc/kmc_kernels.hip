@@ -78,6 +78,8 @@ struct Dev {
   SList plist;          // units with conflict entries (u, 0)
   SList rej;            // units rejected this step (u, 0)
   SList pairs;          // reaction candidates (receptor, partner)
+  int32_t* pq_units;    // [N] units still pending after the grid round (k_col_units)
+  int2* pq_ent;         // [conf capacity] their conflict entries (k_col_compact)
   uint32_t* shard_cnt;  // [5][NSHARD] counters of the lists above
   int2* rank;           // [N] rank of the old / proposed record within its cell
   int32_t* obs_part;    // [blocks][8] per-block observable partials
@@ -2332,7 +2334,11 @@ __global__ void k_col_round(KParams P, Dev d, int round) {
   const uint32_t rt = round_tag(step, round);
   __shared__ uint32_t pre[NSHARD + 1];
   const uint32_t n = sl_prefix(d.conf, pre);
-  if (blockIdx.x == 0 && threadIdx.x == 0) d.ctl->n_pend = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    d.ctl->n_pend = 0;
+    d.ctl->n_pqu = 0;
+    d.ctl->n_pqe = 0;
+  }
   for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x)
     conf_entry(d, sl_at(d.conf, pre, t), step, rt);
 }
@@ -2343,26 +2349,43 @@ __global__ void k_col_units(KParams P, Dev d, int round) {
   __shared__ uint32_t pre[NSHARD + 1];
   const uint32_t n = sl_prefix(d.plist, pre);
   int pend = 0;
-  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x)
-    pend += conf_unit(d, sl_at(d.plist, pre, t).x, step, rt);
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+    const int u = sl_at(d.plist, pre, t).x;
+    if (conf_unit(d, u, step, rt)) {  // still pending: the tail's unit list
+      ++pend;
+      d.pq_units[wave_slot(&d.ctl->n_pqu)] = u;
+    }
+  }
   if (pend) atomicAdd(&d.ctl->n_pend, (uint32_t)pend);
 }
 
-// single workgroup: the remaining rounds, until nothing is pending
+// the conflict entries of the units still pending after the grid round: the
+// only ones later rounds can change (an entry of a decided unit is inert)
+__global__ void k_col_compact(KParams P, Dev d) {
+  if (d.ctl->n_pend == 0) return;
+  const uint32_t step = d.ctl->step;
+  __shared__ uint32_t pre[NSHARD + 1];
+  const uint32_t n = sl_prefix(d.conf, pre);
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+    const int2 e = sl_at(d.conf, pre, t);
+    if (state_of(d, e.x, step) == S_PEND) d.pq_ent[wave_slot(&d.ctl->n_pqe)] = e;
+  }
+}
+
+// single workgroup: the remaining rounds on the compacted pending entries and
+// units (k_col_units, k_col_compact), until nothing is pending
 __global__ void __launch_bounds__(1024) k_col_tail(KParams P, Dev d, int round0) {
   __shared__ uint32_t npend;
   if (d.ctl->n_pend == 0) return;
   const uint32_t step = d.ctl->step;
-  __shared__ uint32_t pre_c[NSHARD + 1], pre_u[NSHARD + 1];
-  const uint32_t n = sl_prefix(d.conf, pre_c);
-  const uint32_t nu = sl_prefix(d.plist, pre_u);
+  const uint32_t n = d.ctl->n_pqe, nu = d.ctl->n_pqu;
   for (int round = round0;; ++round) {
     const uint32_t rt = round_tag(step, round);
     if (threadIdx.x == 0) npend = 0;
-    for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) conf_entry(d, sl_at(d.conf, pre_c, t), step, rt);
+    for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) conf_entry(d, d.pq_ent[t], step, rt);
     __syncthreads();
     int pend = 0;
-    for (uint32_t t = threadIdx.x; t < nu; t += blockDim.x) pend += conf_unit(d, sl_at(d.plist, pre_u, t).x, step, rt);
+    for (uint32_t t = threadIdx.x; t < nu; t += blockDim.x) pend += conf_unit(d, d.pq_units[t], step, rt);
     if (pend) atomicAdd(&npend, (uint32_t)pend);
     __syncthreads();
     if (npend == 0) break;
