@@ -680,7 +680,7 @@ static int launch_step(kmc_sim* s, bool re_sort) {
   Dev& d = s->d;
   hipStream_t st = s->stream;
   const int T = 256;
-  const int gN = (K.N + T - 1) / T, gA = (K.NA + T - 1) / T, gB = (K.NB + T - 1) / T;
+  const int gN = (K.N + T - 1) / T, gB = (K.NB + T - 1) / T;
   s->tnow = s->tmask && (s->tcount++ % s->tperiod) == 0;
   if (s->tnow) harvest(s, s->tslot);  // the slot's previous use is TRING bracketed steps old
   if (re_sort) {

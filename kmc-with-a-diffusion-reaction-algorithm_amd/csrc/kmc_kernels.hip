@@ -1915,27 +1915,22 @@ __device__ __forceinline__ void wg_flush(WgList& L, const SList& out, uint32_t* 
 // halo into LDS as 2·halo segments (one per halo row and kind; each one
 // contiguous range of the sorted array, all loads in flight at once) and tags
 // every staged record with its (segment, column).  Every scanning record of
-// the block then writes the LDS indices of the records in its cut stencil —
+// the block then takes the LDS indices of the records in its cut stencil —
 // per neighbour kind, only the cells within that kind pair's reach of the
 // record (its offset inside its cell decides which side columns / rows can
-// hold a partner) — into an LDS pair list (one wave-level prefix sum + one
-// LDS atomic per wave), and the pairs are checked with every lane busy.  A
-// record whose pairs do not fit the list is scanned in place.
+// hold a partner) — as six LDS index ranges, and each wave walks its records'
+// pairs with every lane busy (tile_walk).
 #define TILE_MAX 14
 #define HALO_MAX (TILE_MAX + 2)
 #define NSEG_MAX (2 * HALO_MAX)
 #define TCAP 768
-#define PCAP 2048
-#define PAIR_NONE 0xffffffffu
 struct TileLds {
   float4 pos[TCAP];
   int2 id[TCAP];
   uint16_t tag[TCAP];                  // segment | column << 8 of each staged record
-  uint32_t pair[PCAP];                 // scanning record | neighbour record << 16 (LDS indices)
   int cstart[NSEG_MAX][HALO_MAX + 1];  // segment = halo row * 2 + kind: LDS index of each cell's first record; [seg][halo] = end
   int goff[NSEG_MAX];                  // global record index − LDS index, per segment
   int n;
-  uint32_t npair;
 };
 
 __device__ __forceinline__ int cell_index(const KParams& P, int cx, int cy, int kind) {
@@ -1952,7 +1947,6 @@ __device__ bool tile_load(const KParams& P, const Dev& d, int tx, int ty, TileLd
   const int tile = P.tile, halo = tile + 2, nseg = 2 * halo;
   const int cx0 = tx * tile - 1, cy0 = ty * tile - 1;
   const int xlo = max(cx0, 0), xhi = min(cx0 + halo - 1, P.ncx - 1);
-  if (threadIdx.x == 0) T.npair = 0;
   for (int idx = threadIdx.x; idx < nseg * (halo + 1); idx += blockDim.x) {
     int seg = idx / (halo + 1), hx = idx - seg * (halo + 1);
     int y = cy0 + (seg >> 1);
@@ -2036,47 +2030,60 @@ __device__ __forceinline__ void item_ranges(const KParams& P, const TileLds& T, 
   }
 }
 
-// Pair list of the block: rng(l, seg, hx, r0, r1) gives the six ranges
-// (kind 0 rows, kind 1 rows) of a scanning record l, or false;
-// ovf(l, r0, r1) scans a record whose pairs do not fit.  All threads call;
-// ends with a barrier.
-template <class Rng, class Ovf>
-__device__ __forceinline__ void tile_pairs(const KParams& P, TileLds& T, Rng rng, Ovf ovf) {
+// Pairs of the block, without a pair list: rng(l, seg, hx, r0, r1) gives the
+// six ranges (kind 0 rows, kind 1 rows) of a scanning record l, or false.
+// Every lane of a wave holds one record's ranges; the wave walks the
+// concatenation of its lanes' ranges 64 pairs at a time — lane L takes pair
+// j + L, finds its owner lane by a binary search over the lanes' inclusive
+// prefix and its neighbour record from the owner's packed range starts — so
+// every lane checks a pair, the owner's record is a broadcast LDS read and the
+// neighbour records of consecutive lanes are mostly consecutive.
+// chk(l, r) for every pair; all threads call (no barrier).
+template <class Rng, class Chk>
+__device__ __forceinline__ void tile_walk(const KParams& P, const TileLds& T, Rng rng, Chk chk) {
   const int tile = P.tile, n = T.n, lane = __lane_id();
   for (int base = 0; base < n; base += blockDim.x) {
     const int l = base + threadIdx.x;
     int r0[6], r1[6];
     bool item = false;
-    int tot = 0;
     if (l < n) {
       const int tg = T.tag[l], seg = tg & 0xff, hx = tg >> 8, hy = seg >> 1;
       if (hy >= 1 && hy <= tile && hx >= 1 && hx <= tile) item = rng(l, seg, hx, r0, r1);
-      if (item)
-#pragma unroll
-        for (int k = 0; k < 6; ++k) tot += r1[k] - r0[k];
     }
-    int inc = tot;  // wave-level prefix sum (every lane of the wave is here)
+    // range starts | pairs before the range << 16 (LDS indices < TCAP, counts < 6 TCAP)
+    uint32_t pk[6];
+    int tot = 0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const int len = item ? r1[k] - r0[k] : 0;
+      pk[k] = (uint32_t)(item ? r0[k] : 0) | (uint32_t)tot << 16;
+      tot += len;
+    }
+    int inc = tot;  // wave-level inclusive prefix (every lane of the wave is here)
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-      int t = __shfl_up(inc, o, 64);
+      const int t = __shfl_up(inc, o, 64);
       if (lane >= o) inc += t;
     }
-    const int wtot = __shfl(inc, 63, 64);
-    uint32_t wbase = 0;
-    if (lane == 0 && wtot) wbase = atomicAdd(&T.npair, (uint32_t)wtot);
-    wbase = __shfl(wbase, 0, 64);
-    if (!item) continue;
-    uint32_t off = wbase + (uint32_t)(inc - tot);
-    if (off + tot <= PCAP) {
+    const int excl = inc - tot, wtot = __shfl(inc, 63, 64);
+    const int l0 = l - lane;
+    for (int j = 0; j < wtot; j += 64) {
+      const int q = j + lane;
+      int o = 0;  // owner: the number of lanes whose inclusive prefix is <= q
 #pragma unroll
-      for (int k = 0; k < 6; ++k)
-        for (int r = r0[k]; r < r1[k]; ++r) T.pair[off++] = (uint32_t)l | (uint32_t)r << 16;
-    } else {
-      for (uint32_t s = off; s < min(off + (uint32_t)tot, (uint32_t)PCAP); ++s) T.pair[s] = PAIR_NONE;
-      ovf(l, r0, r1);
+      for (int s = 32; s; s >>= 1)
+        if (__shfl(inc, o + s - 1, 64) <= q) o += s;
+      o = min(o, 63);
+      const int t = q - __shfl(excl, o, 64);
+      uint32_t sel = __shfl(pk[0], o, 64);
+#pragma unroll
+      for (int k = 1; k < 6; ++k) {
+        const uint32_t v = __shfl(pk[k], o, 64);
+        if ((int)(v >> 16) <= t) sel = v;
+      }
+      if (q < wtot) chk(l0 + o, (int)(sel & 0xffffu) + t - (int)(sel >> 16));
     }
   }
-  __syncthreads();
 }
 
 // Up to four (a, b) entries held in registers per lane while pairs are
@@ -2192,7 +2199,9 @@ __global__ void __launch_bounds__(256) k_col_scan(KParams P, Dev d) {
   if (tile_load(P, d, tx, ty, T, nullptr, 0, S)) {
     if (P.dbg_stage == 1) return;
     // proposal records and their cut stencils
-    tile_pairs(
+    PairBuf B;
+    B.n = 0;
+    tile_walk(
         P, T,
         [&](int l, int seg, int hx, int* r0, int* r1) {
           const int2 me = T.id[l];
@@ -2207,32 +2216,14 @@ __global__ void __launch_bounds__(256) k_col_scan(KParams P, Dev d) {
           item_ranges(P, T, tx, ty, seg, hx, mp.x, mp.y, 1, mA ? REACH_AB : REACH_BB, r0 + 3, r1 + 3);
           return true;
         },
-        [&](int l, const int* r0, const int* r1) {
-          const int2 me = T.id[l];
-          const float4 mp = T.pos[l];
-          for (int k = 0; k < 6; ++k)
-            for (int r = r0[k]; r < r1[k]; ++r) {
-              const int2 id = T.id[r];
-              if (!col_pair(NA, me, mp, id, T.pos[r])) continue;
-              if (id.y < 0) atomicOr(&d.ctl->err, ERR_RESOLVE);
-              else col_emit(d, L, tile_global(T, l), tile_global(T, r));
-            }
+        [&](int il, int nl) {
+          const int2 id = T.id[nl];
+          if (!col_pair(NA, T.id[il], T.pos[il], id, T.pos[nl])) return;
+          if (id.y < 0) atomicOr(&d.ctl->err, ERR_RESOLVE);
+          else if (B.n < 4) pair_push(B, make_int2(il, nl));
+          else col_emit(d, L, tile_global(T, il), tile_global(T, nl));
         });
     S(d, 5);
-    if (P.dbg_stage == 2) return;
-    const uint32_t np = min(T.npair, (uint32_t)PCAP);
-    PairBuf B;
-    B.n = 0;
-    for (uint32_t p = threadIdx.x; p < np; p += blockDim.x) {
-      const uint32_t e = T.pair[p];
-      if (e == PAIR_NONE) continue;
-      const int il = e & 0xffff, nl = e >> 16;
-      const int2 id = T.id[nl];
-      if (!col_pair(NA, T.id[il], T.pos[il], id, T.pos[nl])) continue;
-      if (id.y < 0) atomicOr(&d.ctl->err, ERR_RESOLVE);
-      else if (B.n < 4) pair_push(B, make_int2(il, nl));
-      else col_emit(d, L, tile_global(T, il), tile_global(T, nl));
-    }
     pair_flush(B, L, d.cand, &d.ctl->err,
                [&](int2 v) { return make_int2(tile_global(T, v.x), tile_global(T, v.y)); });
     S(d, 6);
@@ -2499,7 +2490,9 @@ __global__ void __launch_bounds__(256) k_rxn_scan_tile(KParams P, Dev d) {
   if (tile_load(P, d, tx, ty, T, site, step, S)) {
     if (P.dbg_stage == 1) return;
     // final receptor records that can still react, and their cut stencils
-    tile_pairs(
+    PairBuf B;
+    B.n = 0;
+    tile_walk(
         P, T,
         [&](int l, int seg, int hx, int* r0, int* r1) {
           const int2 me = T.id[l];
@@ -2513,30 +2506,14 @@ __global__ void __launch_bounds__(256) k_rxn_scan_tile(KParams P, Dev d) {
             for (int k = 3; k < 6; ++k) r1[k] = r0[k];
           return true;
         },
-        [&](int l, const int* r0, const int* r1) {
-          const int2 me = T.id[l];
-          for (int k = 0; k < 6; ++k)
-            for (int r = r0[k]; r < r1[k]; ++r) {
-              const int2 id = T.id[r];
-              if (rxn_pair(NA, me, T.pos[l], site[l], id, T.pos[r], site[r]) && (id.x & RID_FIN))
-                rxn_emit(d, L, me.x & RID_PID, id.x & RID_PID);
-            }
+        [&](int il, int nl) {
+          const int2 me = T.id[il], id = T.id[nl];
+          if (!(rxn_pair(NA, me, T.pos[il], site[il], id, T.pos[nl], site[nl]) && (id.x & RID_FIN))) return;
+          const int2 v = make_int2(me.x & RID_PID, id.x & RID_PID);
+          if (B.n < 4) pair_push(B, v);
+          else rxn_emit(d, L, v.x, v.y);
         });
     S(d, 5);
-    if (P.dbg_stage == 2) return;
-    const uint32_t np = min(T.npair, (uint32_t)PCAP);
-    PairBuf B;
-    B.n = 0;
-    for (uint32_t p = threadIdx.x; p < np; p += blockDim.x) {
-      const uint32_t e = T.pair[p];
-      if (e == PAIR_NONE) continue;
-      const int il = e & 0xffff, nl = e >> 16;
-      const int2 me = T.id[il], id = T.id[nl];
-      if (!(rxn_pair(NA, me, T.pos[il], site[il], id, T.pos[nl], site[nl]) && (id.x & RID_FIN))) continue;
-      const int2 v = make_int2(me.x & RID_PID, id.x & RID_PID);
-      if (B.n < 4) pair_push(B, v);
-      else rxn_emit(d, L, v.x, v.y);
-    }
     pair_flush(B, L, d.pairs, &d.ctl->err, [](int2 v) { return v; });
     S(d, 6);
     if (P.dbg_stage == 3) return;

@@ -14,7 +14,7 @@ state=/tmp/kmc_probe_$wl.kmc
 cd "$root"
 timeout -k 10 400 python bench.py --workload $wl --steps 10 --warmup 0 --no-cpu-baseline --no-fresh-window \
   --save-state $state > "$out/evolve.json" 2> "$out/evolve.err"
-for st in 1 2 3 0; do
+for st in ${STAGES:-1 2 3 0}; do
   KMC_DEBUG_SCAN_STAGE=$st timeout -k 10 200 python bench.py --workload $wl --load-state $state --steps 40 \
     --warmup 105 --no-cpu-baseline --profile > "$out/stage$st.json" 2> "$out/stage$st.err" || true
 done
