@@ -33,7 +33,9 @@ namespace kmcd {
 // b % NSHARD, which owns data[shard·cap, (shard+1)·cap).  One device-scope
 // word sustains only ≈90 atomics/µs (MI355X_MICROARCH.md, dequeue / fan-in),
 // so thousands of workgroups appending to one counter would serialise.
+#ifndef NSHARD  // counter shards per list, a power of two <= 64 (sl_prefix scans them in one wave)
 #define NSHARD 32
+#endif
 struct SList {
   int2* data;
   uint32_t* cnt;  // [NSHARD]
@@ -79,7 +81,7 @@ struct Dev {
   SList rej;            // units rejected this step (u, 0)
   SList pairs;          // reaction candidates (receptor, partner)
   int32_t* pq_units;    // [N] units still pending after the grid round (k_col_units)
-  int2* pq_ent;         // [conf capacity] their conflict entries (k_col_compact)
+  int2* pq_ent;         // [conf capacity] conflict entries left pending by round 0 (k_col_round)
   uint32_t* shard_cnt;  // [5][NSHARD] counters of the lists above
   int2* rank;           // [N] rank of the old / proposed record within its cell
   int32_t* obs_part;    // [blocks][8] per-block observable partials
@@ -1920,10 +1922,14 @@ __device__ __forceinline__ void wg_flush(WgList& L, const SList& out, uint32_t* 
 // record (its offset inside its cell decides which side columns / rows can
 // hold a partner) — as six LDS index ranges, and each wave walks its records'
 // pairs with every lane busy (tile_walk).
+#ifndef TILE_MAX  // (overridable for tile-size sweeps: tools/build_variants.py)
 #define TILE_MAX 14
+#endif
 #define HALO_MAX (TILE_MAX + 2)
 #define NSEG_MAX (2 * HALO_MAX)
+#ifndef TCAP
 #define TCAP 768
+#endif
 struct TileLds {
   float4 pos[TCAP];
   int2 id[TCAP];
@@ -2169,12 +2175,6 @@ __device__ __forceinline__ bool col_pair(int NA, int2 me, float4 mp, int2 id, fl
   return (q != m) & own_ok & prefilter(m < NA, mp.x, mp.y, mp.z, mp.w, q < NA, rp);
 }
 
-struct GlbRecs {
-  const Rec* rec;
-  __device__ float4 p(int r) const { return rec[r].pos; }
-  __device__ int2 id(int r) const { return rec[r].id; }
-};
-
 // one proposal record against three row ranges of records from global memory
 __device__ __forceinline__ void col_scan_glb(const KParams& P, const Dev& d, WgList& L, const int* r0, const int* r1,
                                              int rs, int2 me, float4 mp) {
@@ -2303,13 +2303,18 @@ __global__ void k_col_exact(KParams P, Dev d) {
 // sequential one; the lowest pending key can always decide, so it ends.
 __device__ __forceinline__ uint32_t round_tag(uint32_t step, int round) { return step * 64u + (uint32_t)round; }
 
-__device__ __forceinline__ void conf_entry(const Dev& d, int2 e, uint32_t step, uint32_t rt) {
+// returns true while the entry can still matter: u and kq both pending
+__device__ __forceinline__ bool conf_entry(const Dev& d, int2 e, uint32_t step, uint32_t rt) {
   int u = e.x, kq = e.y & 0x7fffffff;
   bool isnew = e.y < 0;
-  if (state_of(d, u, step) != S_PEND) return;
+  if (state_of(d, u, step) != S_PEND) return false;
   uint32_t sk = state_of(d, kq, step);
-  if (sk == S_PEND) st_state(&d.pend[u], rt);
-  else if ((sk == S_ACC) == isnew) mark_rej(d, u, (step & 0x3fffffffu) << 2);
+  if (sk == S_PEND) {
+    st_state(&d.pend[u], rt);
+    return true;
+  }
+  if ((sk == S_ACC) == isnew) mark_rej(d, u, (step & 0x3fffffffu) << 2);
+  return false;
 }
 
 // returns 1 if u is still pending after this round
@@ -2320,18 +2325,20 @@ __device__ __forceinline__ int conf_unit(const Dev& d, int u, uint32_t step, uin
   return 0;
 }
 
+// Round 0 over every conflict entry.  An entry whose kq is still pending is
+// the only kind a later round can change (an entry evaluated against a
+// decided kq has had its effect), so those are compacted for k_col_tail here.
+// The counters n_pend / n_pqu / n_pqe were zeroed by the previous step's
+// finalisation.
 __global__ void k_col_round(KParams P, Dev d, int round) {
   const uint32_t step = d.ctl->step;
   const uint32_t rt = round_tag(step, round);
   __shared__ uint32_t pre[NSHARD + 1];
   const uint32_t n = sl_prefix(d.conf, pre);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    d.ctl->n_pend = 0;
-    d.ctl->n_pqu = 0;
-    d.ctl->n_pqe = 0;
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+    const int2 e = sl_at(d.conf, pre, t);
+    if (conf_entry(d, e, step, rt)) d.pq_ent[wave_slot(&d.ctl->n_pqe)] = e;
   }
-  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x)
-    conf_entry(d, sl_at(d.conf, pre, t), step, rt);
 }
 
 __global__ void k_col_units(KParams P, Dev d, int round) {
@@ -2350,21 +2357,8 @@ __global__ void k_col_units(KParams P, Dev d, int round) {
   if (pend) atomicAdd(&d.ctl->n_pend, (uint32_t)pend);
 }
 
-// the conflict entries of the units still pending after the grid round: the
-// only ones later rounds can change (an entry of a decided unit is inert)
-__global__ void k_col_compact(KParams P, Dev d) {
-  if (d.ctl->n_pend == 0) return;
-  const uint32_t step = d.ctl->step;
-  __shared__ uint32_t pre[NSHARD + 1];
-  const uint32_t n = sl_prefix(d.conf, pre);
-  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
-    const int2 e = sl_at(d.conf, pre, t);
-    if (state_of(d, e.x, step) == S_PEND) d.pq_ent[wave_slot(&d.ctl->n_pqe)] = e;
-  }
-}
-
 // single workgroup: the remaining rounds on the compacted pending entries and
-// units (k_col_units, k_col_compact), until nothing is pending
+// units (k_col_round, k_col_units), until nothing is pending
 __global__ void __launch_bounds__(1024) k_col_tail(KParams P, Dev d, int round0) {
   __shared__ uint32_t npend;
   if (d.ctl->n_pend == 0) return;
@@ -2390,31 +2384,37 @@ __global__ void __launch_bounds__(1024) k_col_tail(KParams P, Dev d, int round0)
 
 // ================================================================ 5. commit
 // The members of every rejected unit: their final position is the old one.
-// Lanes 0 / 1 move the final flag (RID_FIN) of the member's two records from
-// the proposal record (set by k_rec_scatter) to the old one — the reaction
-// scan reads finality from the records — then R is copied to R_new.
-__device__ __forceinline__ void rej_member(const KParams& P, const Dev& d, int m, uint32_t step, int lane) {
+// The final flag (RID_FIN) of each member's two records moves from the
+// proposal record (set by k_rec_scatter) to the old one — the reaction scan
+// reads finality from the records — then R is copied to R_new.
+// Record w (0 old, 1 proposal) of member m: located from its position in R /
+// R_new (so before R_new is overwritten) and its rank in the cell.
+__device__ __forceinline__ void rej_flag(const KParams& P, const Dev& d, int m, int w) {
   const int NA = P.NA;
-  if (lane < 2) {
-    const Beads& B = lane ? d.nxt : d.cur;
-    const double x = B.P(m, 1, 1, 0), y = B.P(m, 1, 1, 1);
-    const int2 rk = d.rank[m];
-    const int pos = d.cell_start[rec_cell(P, x, y, m >= NA)] + (lane ? rk.y : rk.x);
-    const int st = m < NA ? (A_ST2(d, m) ? RID_ST2 : 0) | (A_ST3(d, m) ? RID_ST3 : 0) : 0;
-    d.rec[pos].id.x = m | st | (lane ? (int)0x80000000 : RID_FIN);
-  }
+  const Beads& B = w ? d.nxt : d.cur;
+  const double x = B.P(m, 1, 1, 0), y = B.P(m, 1, 1, 1);
+  const int2 rk = d.rank[m];
+  const int pos = d.cell_start[rec_cell(P, x, y, m >= NA)] + (w ? rk.y : rk.x);
+  const int st = m < NA ? (A_ST2(d, m) ? RID_ST2 : 0) | (A_ST3(d, m) ? RID_ST3 : 0) : 0;
+  d.rec[pos].id.x = m | st | (w ? (int)0x80000000 : RID_FIN);
+}
+// bead row `row` of member m: R_new = R
+__device__ __forceinline__ void rej_copy(const KParams& P, const Dev& d, int m, int row) {
   const bool a = m < P.NA;
-  const int n = a ? P.NA : P.NB, i = a ? m : m - P.NA, rows = a ? ROWS_A : ROWS_B;
+  const int n = a ? P.NA : P.NB, i = a ? m : m - P.NA;
+  if (row >= (a ? ROWS_A : ROWS_B)) return;
   const double2* src = reinterpret_cast<const double2*>(a ? d.cur.a : d.cur.b);
   double2* dst = reinterpret_cast<double2*>(a ? d.nxt.a : d.nxt.b);
-  if (lane < rows) dst[(size_t)lane * n + i] = src[(size_t)lane * n + i];  // R_new = R
+  dst[(size_t)row * n + i] = src[(size_t)row * n + i];
 }
 
-// one wave per rejected unit: its members get this step's reject tag (their
-// final position is the old one) and copy R -> R_new, one bead row per lane
+// One wave per rejected unit; its lanes take the (member, record) flag moves,
+// then the (member, bead row) copies, of all members at once, so a complex
+// costs the same few dependent loads as a single protein.  Every flag move of
+// the wave reads R_new before any of its copies writes it (program order, and
+// each move's store depends on its loads).
 __global__ void k_rej_commit(KParams P, Dev d) {
   const int NA = P.NA;
-  const uint32_t step = d.ctl->step;
   __shared__ uint32_t pre[NSHARD + 1];
   const uint32_t n = sl_prefix(d.rej, pre);
   const int lane = threadIdx.x & 63;
@@ -2422,13 +2422,17 @@ __global__ void k_rej_commit(KParams P, Dev d) {
   for (uint32_t t = w0; t < n; t += nw) {
     const int sl = d.slot_of[sl_at(d.rej, pre, t).x];
     const uint8_t kind = d.ukind[sl];
+    int off = 0, nm = 1, q = -1;
     if (kind == U_COMPLEX) {
-      const int lb = sl - NA, off = d.cx_off[lb], cs = d.cx_size[lb];
-      for (int k = 0; k < cs; ++k) rej_member(P, d, d.members[off + k], step, lane);
-    } else {
-      rej_member(P, d, sl, step, lane);
-      if (kind == U_DIMER) rej_member(P, d, A_NEI3(d, sl) - 1, step, lane);
+      off = d.cx_off[sl - NA];
+      nm = d.cx_size[sl - NA];
+    } else if (kind == U_DIMER) {
+      nm = 2;
+      q = A_NEI3(d, sl) - 1;
     }
+    auto member = [&](int k) { return kind == U_COMPLEX ? d.members[off + k] : (k ? q : sl); };
+    for (int e = lane; e < 2 * nm; e += 64) rej_flag(P, d, member(e >> 1), e & 1);
+    for (int e = lane; e < nm * ROWS_A; e += 64) rej_copy(P, d, member(e / ROWS_A), e % ROWS_A);
   }
 }
 
@@ -2595,6 +2599,7 @@ __global__ void k_rxn_exact(KParams P, Dev d) {
     }
   }
 }
+
 
 // ---------------------------------------------------------------- greedy
 // In-place bitonic sort of keys[0..np) (np a power of two) by one workgroup.
@@ -2908,11 +2913,11 @@ __global__ void __launch_bounds__(256) k_finalize(KParams P, Dev d, double time_
   if ((threadIdx.x & 63) == 0)
     for (int f = 0; f < 6; ++f) red[threadIdx.x >> 6][f] = v[f];
   __syncthreads();
-  if (threadIdx.x < 5 * NSHARD) {  // lists in shard_cnt order: cand conf plist rej pairs
-    const int l = threadIdx.x / NSHARD;
+  for (int k = threadIdx.x; k < 5 * NSHARD; k += blockDim.x) {  // lists in shard_cnt order: cand conf plist rej pairs
+    const int l = k / NSHARD;
     const uint32_t cap = l == 0 ? d.cand.cap : l == 1 ? d.conf.cap : l == 2 ? d.plist.cap : l == 3 ? d.rej.cap : d.pairs.cap;
-    atomicAdd(&tot[l], min(d.shard_cnt[threadIdx.x], cap));
-    d.shard_cnt[threadIdx.x] = 0;
+    atomicAdd(&tot[l], min(d.shard_cnt[k], cap));
+    d.shard_cnt[k] = 0;
   }
   __syncthreads();
   if (threadIdx.x != 0) return;
@@ -2949,6 +2954,8 @@ __global__ void __launch_bounds__(256) k_finalize(KParams P, Dev d, double time_
   c->n_dirty[(step + 1) & 1] = 0;  // consumed by this step's k_cx_kill; the next step's reactions fill it
   c->n_heavy = 0;
   c->n_pend = 0;
+  c->n_pqu = 0;  // filled by the next step's k_col_round / k_col_units
+  c->n_pqe = 0;
   c->n_rl = 0;
   c->n_cisc = 0;
 }

@@ -149,6 +149,24 @@ def test_exact_state_resume(tmp_path):
     assert o.hash() == h_a
 
 
+@pytest.mark.parametrize("graph", ["0", "1"])
+def test_graph_replay_dense(monkeypatch, graph):
+    # KMC_GRAPH=1: plain steps replay captured HIP graphs (one per buffer
+    # parity; re-sorts every 7 steps force eager steps and fresh captures in
+    # between); KMC_GRAPH=0: every step launched eagerly
+    monkeypatch.setenv("KMC_GRAPH", graph)
+    monkeypatch.setenv("KMC_RESORT", "7")
+    p = params(seed=37, **DENSE)
+    o = O.Oracle(p)
+    o.init_placement()
+    sim = engine.Simulation(p)
+    sim.set_state(o.get_state())
+    obs = np.concatenate([sim.step(n) for n in (1, 2, 997, 500)])
+    obs_o, _ = o.step(1500, want_hashes=False)
+    assert np.array_equal(obs, obs_o)
+    assert engine.state_hash(p, sim.get_state()) == o.hash()
+
+
 def test_chunked_steps_equal_single_steps():
     p = params(seed=3, **DENSE)
     o = O.Oracle(p)
