@@ -59,13 +59,11 @@ def kernel_bytes(name: str, n_a: int, n_b: int):
         # receptor / 8 ligand beads × xyz × 8 B) and R_new written, its unit
         # kind read, its record ranks written
         "k_propose": 768 * n_a + 384 * n_b + n + 8 * n,
-        # every record once (float4 + id)
-        "k_col_scan": 2 * n * 24,
+        # every record once (float4 + id + site)
+        "k_pair_scan": 2 * n * 32,
         # old + new reference points (x, y, zlo, zhi) + receptor site, record
         # write (pos, id, site), owner, cell cursor
         "k_rec_scatter": 2 * n * 32 + 2 * n_a * 16 + 2 * n * 32 + 4 * n + 2 * n * 8,
-        # every record once (float4 + id + site) + final flags
-        "k_rxn_scan": 2 * n * 32 + n,
         "k_commit": 8 * n,
         "k_classify": 20 * n_a + 12 * n_b + 5 * n,
         "k_observe": 16 * n_a + 5 * n_b,
@@ -98,7 +96,7 @@ def pmc_traffic(kernel: str, workload: str):
 
 def kernel_trace_name(name: str) -> str:
     # engine timing names -> the kernel symbol rocprof reports
-    return {"k_rxn_scan": "k_rxn_scan_tile"}.get(name, name)
+    return {"k_commit": "k_rej_commit"}.get(name, name)
 
 
 def parse(argv):

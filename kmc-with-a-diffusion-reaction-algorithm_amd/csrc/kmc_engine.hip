@@ -21,13 +21,13 @@ using namespace kmcd;
 enum KId {
   KI_CLASSIFY, KI_BFS, KI_PROPOSE, KI_PROPOSE_FREE, KI_MOVE_MEMBERS, KI_COMPLEX, KI_CX_CHECK, KI_CX_HEAVY, KI_CX_KILL, KI_SCAN,
   KI_REC_SCATTER,
-  KI_COL_SCAN, KI_COL_EXACT, KI_COL_ROUNDS, KI_COMMIT, KI_RXN_SCAN, KI_RXN_EXACT, KI_MATCH, KI_DISS_OBSERVE,
+  KI_PAIR_SCAN, KI_COL_EXACT, KI_COL_ROUNDS, KI_COMMIT, KI_RXN_EXACT, KI_MATCH, KI_DISS_OBSERVE,
   KI_RESORT, KI_N
 };
 static const char* const KNAMES[KI_N] = {
     "k_classify", "k_bfs", "k_propose", "k_propose_free", "k_move_members", "k_cx_params", "k_cx_check", "k_complex_heavy",
     "k_cx_kill", "k_scan",
-    "k_rec_scatter", "k_col_scan", "k_col_exact", "k_col_rounds", "k_commit", "k_rxn_scan", "k_rxn_exact",
+    "k_rec_scatter", "k_pair_scan", "k_col_exact", "k_col_rounds", "k_commit", "k_rxn_exact",
     "k_match", "k_diss_observe", "slot_resort"};
 #define TRING 64  // steps of event pairs kept in flight
 
@@ -748,7 +748,8 @@ static int launch_step(kmc_sim* s, bool re_sort) {
   TIMED(KI_REC_SCATTER, (k_rec_scatter<<<gN, T, 0, st>>>(K, d)));
   const int gX = std::min(2048, (K.N + T - 1) / T);  // grid-stride kernels over device-sized lists
   const int ntiles = ((K.ncx + K.tile - 1) / K.tile) * ((K.ncy + K.tile - 1) / K.tile);
-  TIMED(KI_COL_SCAN, (k_col_scan<<<ntiles, 256, 0, st>>>(K, d)));
+  // collision candidates and reaction candidates, one staging of each tile
+  TIMED(KI_PAIR_SCAN, (k_pair_scan<<<ntiles, 256, 0, st>>>(K, d)));
   TIMED(KI_COL_EXACT, (k_col_exact<<<gX, T, 0, st>>>(K, d)));
   TIMED(KI_COL_ROUNDS, {
     k_col_round<<<gX, T, 0, st>>>(K, d, 0);
@@ -757,7 +758,6 @@ static int launch_step(kmc_sim* s, bool re_sort) {
   });
   TIMED(KI_COMMIT, (k_rej_commit<<<gX, T, 0, st>>>(K, d)));
   if (K.NA > 0) {
-    TIMED(KI_RXN_SCAN, (k_rxn_scan_tile<<<ntiles, 256, 0, st>>>(K, d)));
     TIMED(KI_RXN_EXACT, (k_rxn_exact<<<1024, T, 0, st>>>(K, d)));
     TIMED(KI_MATCH, (k_match<<<1, 1024, 0, st>>>(K, d)));
   }

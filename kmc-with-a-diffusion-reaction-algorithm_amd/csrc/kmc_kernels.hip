@@ -1388,8 +1388,8 @@ __device__ __forceinline__ void cx_rigid(const KParams& P, const Dev& d, CxLds* 
 //                  and the centre of mass (sums over the members' [1][1] and
 //                  [j][1] beads in BFS member order, 994-1067), the rotation
 //                  matrix -> cxp[root] (16 doubles)
-//   k_propose_units  (a member's thread) every bead moved with its complex's
-//                  parameters — the same expressions as the wave version
+//   k_move_members (a member's thread) every bead moved with its complex's
+//                  parameters — the same expressions as the heavy path's
 //   k_cx_check     one thread per complex: the lay-down / alignment tests
 //                  (1141, 1215, 1255) on R_new; a complex that passes has its
 //                  members' new records counted, any other (a test fails, or
@@ -2188,74 +2188,6 @@ __device__ __forceinline__ void col_scan_glb(const KParams& P, const Dev& d, WgL
     }
 }
 
-__global__ void __launch_bounds__(256) k_col_scan(KParams P, Dev d) {
-  __shared__ TileLds T;
-  __shared__ WgList L;
-  const int NA = P.NA;
-  const int ntx = (P.ncx + P.tile - 1) / P.tile;
-  const int tx = blockIdx.x % ntx, ty = blockIdx.x / ntx;
-  wg_list_init(L);
-  Stamper S(0);
-  if (tile_load(P, d, tx, ty, T, nullptr, 0, S)) {
-    if (P.dbg_stage == 1) return;
-    // proposal records and their cut stencils
-    PairBuf B;
-    B.n = 0;
-    tile_walk(
-        P, T,
-        [&](int l, int seg, int hx, int* r0, int* r1) {
-          const int2 me = T.id[l];
-          if (me.x >= 0) return false;
-          if (me.y < 0) {
-            atomicOr(&d.ctl->err, ERR_RESOLVE);
-            return false;
-          }
-          const float4 mp = T.pos[l];
-          const bool mA = (me.x & RID_PID) < NA;
-          item_ranges(P, T, tx, ty, seg, hx, mp.x, mp.y, 0, mA ? REACH_AA : REACH_AB, r0, r1);
-          item_ranges(P, T, tx, ty, seg, hx, mp.x, mp.y, 1, mA ? REACH_AB : REACH_BB, r0 + 3, r1 + 3);
-          return true;
-        },
-        [&](int il, int nl) {
-          const int2 id = T.id[nl];
-          if (!col_pair(NA, T.id[il], T.pos[il], id, T.pos[nl])) return;
-          if (id.y < 0) atomicOr(&d.ctl->err, ERR_RESOLVE);
-          else if (B.n < 4) pair_push(B, make_int2(il, nl));
-          else col_emit(d, L, tile_global(T, il), tile_global(T, nl));
-        });
-    S(d, 5);
-    pair_flush(B, L, d.cand, &d.ctl->err,
-               [&](int2 v) { return make_int2(tile_global(T, v.x), tile_global(T, v.y)); });
-    S(d, 6);
-    if (P.dbg_stage == 3) return;
-    wg_flush(L, d.cand, &d.ctl->err);
-    S(d, 7);
-    return;
-  }
-  // dense tile: one thread per interior cell, records from global memory
-  for (int c = threadIdx.x; c < P.tile * P.tile; c += blockDim.x) {
-    int x = tx * P.tile + c % P.tile, y = ty * P.tile + c / P.tile;
-    if (x >= P.ncx || y >= P.ncy) continue;
-    int ra[3], rb[3], sa[3], sb[3];
-    cell_ranges(P, d, x, y, 0, ra, sa);
-    cell_ranges(P, d, x, y, 1, rb, sb);
-    for (int kind = 0; kind < 2; ++kind) {
-      int s0 = d.cell_start[cell_index(P, x, y, kind)], s1 = d.cell_start[cell_index(P, x + 1, y, kind)];
-      for (int r = s0; r < s1; ++r) {
-        int2 me = d.rec[r].id;
-        if (me.x >= 0) continue;
-        if (me.y < 0) {
-          atomicOr(&d.ctl->err, ERR_RESOLVE);
-          continue;
-        }
-        col_scan_glb(P, d, L, ra, sa, r, me, d.rec[r].pos);
-        col_scan_glb(P, d, L, rb, sb, r, me, d.rec[r].pos);
-      }
-    }
-  }
-  wg_flush(L, d.cand, &d.ctl->err);
-}
-
 // ---------------------------------------------------------------- 4b. exact
 // u rejected; the first to reject it lists it for the commit
 __device__ __forceinline__ void mark_rej(const Dev& d, int u, uint32_t tag) {
@@ -2437,109 +2369,150 @@ __global__ void k_rej_commit(KParams P, Dev d) {
 }
 
 // ================================================================ 6. reactions
-__device__ __forceinline__ bool record_final(const Dev& d, int2 id, uint32_t step) {
-  return (id.x & RID_FIN) != 0;
+// Reaction candidates (main.cpp:1877-2058): a receptor that can still react
+// (not both bonds taken) is paired with the receptors (cis) and ligands (R–L)
+// near it.  The reference pairs FINAL positions, which are known only after
+// the collision resolution; the pair scan below runs before it and pairs
+// every record of such a receptor (old and proposed) with every record near
+// it, with conservative single-precision prefilters (R–L: ligand centre within
+// reach of the [3][2] site; cis: the two [3][3] sites within 16 Å).  Exactly
+// one of a protein's two records is final (RID_FIN, moved by k_rej_commit),
+// so of the up to four record combinations of a protein pair at most one is
+// final-final: k_rxn_exact keeps that one — the same pairs as a scan of the
+// final records.
+__device__ __forceinline__ void rxn_emit(const Dev& d, WgList& L, int a, int b) {
+  wg_emit(L, make_int2(a, b), d.pairs, &d.ctl->err);
 }
 
-// Reaction candidates, pass 1 (tiled): the final-position record of every
-// receptor that can still react is paired with the final records in its cut
-// stencil (cis: receptors within 58 Å, R–L: ligands within 106 Å) and checked
-// with conservative single-precision prefilters (R–L: ligand centre within
-// reach of the [3][2] site; cis: the two [3][3] sites within 16 Å); passing
-// (receptor, partner) pairs go to the exact gates of pass 2.  Record sites and
-// final flags are staged in LDS with the tile.
-__device__ __forceinline__ void rxn_emit(const Dev& d, WgList& L, int i, int q) {
-  wg_emit(L, make_int2(i, q), d.pairs, &d.ctl->err);
+// the receptor of record `me` can take part in a reaction (either bond free)
+__device__ __forceinline__ bool rxn_item(int NA, int2 me) {
+  return (me.x & RID_PID) < NA && !((me.x & RID_ST2) && (me.x & RID_ST3));
 }
 
-// prefilter of one (receptor record, final-candidate record) pair
+// prefilter of one (receptor record, record) pair, finality aside
 __device__ __forceinline__ bool rxn_pair(int NA, int2 me, float4 mp, float2 ms, int2 id, float4 rp, float2 qs) {
   const int i = me.x & RID_PID, q = id.x & RID_PID;
   const bool isB = q >= NA;
   const float dx = rp.x - mp.x, dy = rp.y - mp.y;
   const float dxy2 = dx * dx + dy * dy;
-  const bool rl_ok = isB & (dxy2 < 105.0f * 105.0f) & (rp.z > mp.z - 85.0f) & (rp.z < mp.w + 85.0f);
+  const bool rl_ok = isB & !(me.x & RID_ST2) & (dxy2 < 105.0f * 105.0f) & (rp.z > mp.z - 85.0f) &
+                     (rp.z < mp.w + 85.0f);
   const float gap = fmaxf(fmaxf(rp.z - mp.w, mp.z - rp.w), 0.0f);
   const float tx = qs.x - ms.x, ty = qs.y - ms.y;
-  const bool cis_ok = !isB & !(id.x & RID_ST3) & (dxy2 < 57.0f * 57.0f) & (gap < 16.0f) &
+  const bool cis_ok = !isB & !(me.x & RID_ST3) & !(id.x & RID_ST3) & (dxy2 < 57.0f * 57.0f) & (gap < 16.0f) &
                       (tx * tx + ty * ty < 16.0f * 16.0f);
   return (q != i) & (rl_ok | cis_ok);
 }
 
 // one receptor record against three row ranges, records from global memory
 __device__ __forceinline__ void rxn_scan_glb(const KParams& P, const Dev& d, WgList& L, const int* r0, const int* r1,
-                                             int2 me, float4 mp, float2 ms, uint32_t step) {
-  const bool want_rl = !(me.x & RID_ST2) && P.NB > 0, want_cis = !(me.x & RID_ST3);
+                                             int rs, int2 me, float4 mp, float2 ms) {
 #pragma unroll
   for (int k = 0; k < 3; ++k)
-    for (int r = r0[k]; r < r1[k]; ++r) {
-      const int2 id = d.rec[r].id;
-      const int q = id.x & RID_PID;
-      if (!(q >= P.NA ? want_rl : want_cis)) continue;
-      if (!rxn_pair(P.NA, me, mp, ms, id, d.rec[r].pos, d.rec[r].site) || !record_final(d, id, step)) continue;
-      rxn_emit(d, L, me.x & RID_PID, q);
-    }
+    for (int r = r0[k]; r < r1[k]; ++r)
+      if (rxn_pair(P.NA, me, mp, ms, d.rec[r].id, d.rec[r].pos, d.rec[r].site)) rxn_emit(d, L, rs, r);
 }
 
-__global__ void __launch_bounds__(256) k_rxn_scan_tile(KParams P, Dev d) {
+// ---------------------------------------------------------------- pair scan
+// One staging of each tile for both pair searches of the step: collision
+// candidates of the proposal records (pass A, §4a) and reaction candidates of
+// the records of receptors that can react (above).  An item's stencil is cut
+// to the larger of its two reaches per neighbour kind; each pair is tested
+// against both filters.
+__global__ void __launch_bounds__(256) k_pair_scan(KParams P, Dev d) {
   __shared__ TileLds T;
   __shared__ float2 site[TCAP];
-  __shared__ WgList L;
+  __shared__ WgList Lc, Lr;
+  const int NA = P.NA, NB = P.NB;
   const int ntx = (P.ncx + P.tile - 1) / P.tile;
   const int tx = blockIdx.x % ntx, ty = blockIdx.x / ntx;
-  const int NA = P.NA, NB = P.NB;
-  const uint32_t step = d.ctl->step;
-  wg_list_init(L);
-  Stamper S(8);
-  if (tile_load(P, d, tx, ty, T, site, step, S)) {
+  wg_list_init(Lc);
+  wg_list_init(Lr);
+  Stamper S(0);
+  if (tile_load(P, d, tx, ty, T, site, 0, S)) {
     if (P.dbg_stage == 1) return;
-    // final receptor records that can still react, and their cut stencils
-    PairBuf B;
-    B.n = 0;
+    PairBuf Bc, Br;
+    Bc.n = 0;
+    Br.n = 0;
     tile_walk(
         P, T,
         [&](int l, int seg, int hx, int* r0, int* r1) {
           const int2 me = T.id[l];
-          if ((me.x & RID_PID) >= NA || ((me.x & RID_ST2) && (me.x & RID_ST3)) || !(me.x & RID_FIN)) return false;
+          bool prop = me.x < 0;  // proposal record: collision candidates
+          if (prop && me.y < 0) {
+            atomicOr(&d.ctl->err, ERR_RESOLVE);
+            prop = false;
+          }
+          const bool rx = rxn_item(NA, me);
+          if (!prop && !rx) return false;
+          const bool mA = (me.x & RID_PID) < NA;
+          float reach0 = prop ? (mA ? REACH_AA : REACH_AB) : 0.0f;
+          float reach1 = prop ? (mA ? REACH_AB : REACH_BB) : 0.0f;
+          if (rx && !(me.x & RID_ST3)) reach0 = fmaxf(reach0, REACH_CIS);
+          if (rx && !(me.x & RID_ST2) && NB > 0) reach1 = fmaxf(reach1, REACH_RL);
           const float4 mp = T.pos[l];
-          item_ranges(P, T, tx, ty, seg, hx, mp.x, mp.y, 0, REACH_CIS, r0, r1);
-          item_ranges(P, T, tx, ty, seg, hx, mp.x, mp.y, 1, REACH_RL, r0 + 3, r1 + 3);
-          if (me.x & RID_ST3)
+          item_ranges(P, T, tx, ty, seg, hx, mp.x, mp.y, 0, reach0, r0, r1);
+          item_ranges(P, T, tx, ty, seg, hx, mp.x, mp.y, 1, reach1, r0 + 3, r1 + 3);
+          if (reach0 == 0.0f)
             for (int k = 0; k < 3; ++k) r1[k] = r0[k];
-          if ((me.x & RID_ST2) || NB == 0)
+          if (reach1 == 0.0f)
             for (int k = 3; k < 6; ++k) r1[k] = r0[k];
           return true;
         },
         [&](int il, int nl) {
           const int2 me = T.id[il], id = T.id[nl];
-          if (!(rxn_pair(NA, me, T.pos[il], site[il], id, T.pos[nl], site[nl]) && (id.x & RID_FIN))) return;
-          const int2 v = make_int2(me.x & RID_PID, id.x & RID_PID);
-          if (B.n < 4) pair_push(B, v);
-          else rxn_emit(d, L, v.x, v.y);
+          const float4 mp = T.pos[il], rp = T.pos[nl];
+          if (me.x < 0 && me.y >= 0 && col_pair(NA, me, mp, id, rp)) {
+            if (id.y < 0) atomicOr(&d.ctl->err, ERR_RESOLVE);
+            else if (Bc.n < 4) pair_push(Bc, make_int2(il, nl));
+            else col_emit(d, Lc, tile_global(T, il), tile_global(T, nl));
+          }
+          if (rxn_item(NA, me) && rxn_pair(NA, me, mp, site[il], id, rp, site[nl])) {
+            if (Br.n < 4) pair_push(Br, make_int2(il, nl));
+            else rxn_emit(d, Lr, tile_global(T, il), tile_global(T, nl));
+          }
         });
     S(d, 5);
-    pair_flush(B, L, d.pairs, &d.ctl->err, [](int2 v) { return v; });
+    auto glb = [&](int2 v) { return make_int2(tile_global(T, v.x), tile_global(T, v.y)); };
+    pair_flush(Bc, Lc, d.cand, &d.ctl->err, glb);
+    pair_flush(Br, Lr, d.pairs, &d.ctl->err, glb);
     S(d, 6);
     if (P.dbg_stage == 3) return;
-    wg_flush(L, d.pairs, &d.ctl->err);
+    wg_flush(Lc, d.cand, &d.ctl->err);
+    wg_flush(Lr, d.pairs, &d.ctl->err);
     S(d, 7);
     return;
   }
+  // dense tile: one thread per interior cell, records from global memory
   for (int c = threadIdx.x; c < P.tile * P.tile; c += blockDim.x) {
     int x = tx * P.tile + c % P.tile, y = ty * P.tile + c / P.tile;
     if (x >= P.ncx || y >= P.ncy) continue;
-    int ra[3], sa[3], rb[3], sb[3];
+    int ra[3], rb[3], sa[3], sb[3];
     cell_ranges(P, d, x, y, 0, ra, sa);
     cell_ranges(P, d, x, y, 1, rb, sb);
-    int s0 = d.cell_start[cell_index(P, x, y, 0)], s1 = d.cell_start[cell_index(P, x + 1, y, 0)];
-    for (int r = s0; r < s1; ++r) {
-      int2 me = d.rec[r].id;
-      if (((me.x & RID_ST2) && (me.x & RID_ST3)) || !record_final(d, me, step)) continue;
-      rxn_scan_glb(P, d, L, ra, sa, me, d.rec[r].pos, d.rec[r].site, step);
-      rxn_scan_glb(P, d, L, rb, sb, me, d.rec[r].pos, d.rec[r].site, step);
+    for (int kind = 0; kind < 2; ++kind) {
+      int s0 = d.cell_start[cell_index(P, x, y, kind)], s1 = d.cell_start[cell_index(P, x + 1, y, kind)];
+      for (int r = s0; r < s1; ++r) {
+        const int2 me = d.rec[r].id;
+        const float4 mp = d.rec[r].pos;
+        if (me.x < 0) {
+          if (me.y < 0) {
+            atomicOr(&d.ctl->err, ERR_RESOLVE);
+          } else {
+            col_scan_glb(P, d, Lc, ra, sa, r, me, mp);
+            col_scan_glb(P, d, Lc, rb, sb, r, me, mp);
+          }
+        }
+        if (rxn_item(NA, me)) {
+          const float2 ms = d.rec[r].site;
+          rxn_scan_glb(P, d, Lr, ra, sa, r, me, mp, ms);
+          rxn_scan_glb(P, d, Lr, rb, sb, r, me, mp, ms);
+        }
+      }
     }
   }
-  wg_flush(L, d.pairs, &d.ctl->err);
+  wg_flush(Lc, d.cand, &d.ctl->err);
+  wg_flush(Lr, d.pairs, &d.ctl->err);
 }
 
 // Reaction candidates, pass 2: exact R–L association gates (main.cpp:1880-1921)
@@ -2553,8 +2526,10 @@ __global__ void k_rxn_exact(KParams P, Dev d) {
   __shared__ uint32_t pre[NSHARD + 1];
   const uint32_t n = sl_prefix(d.pairs, pre);
   for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
-    int2 pr = sl_at(d.pairs, pre, t);
-    int i = pr.x, q = pr.y;
+    const int2 pr = sl_at(d.pairs, pre, t);
+    const int2 ra = d.rec[pr.x].id, rb = d.rec[pr.y].id;
+    if (!(ra.x & rb.x & RID_FIN)) continue;  // not both final positions (see the pair scan)
+    const int i = ra.x & RID_PID, q = rb.x & RID_PID;
     if (q >= NA) {
       int lb = q - NA;
       for (int k = 2; k <= 4; ++k) {

@@ -48,9 +48,9 @@ def _evolved_window(p, evolve, window):
 
 @pytest.mark.timeout(600)
 def test_c3_steady_state_window():
-    # C3: 1e6 particles, reference physics, 20 000 steps evolved, 12-step window
+    # C3: 1e6 particles, reference physics, 20 000 steps evolved, 20-step window
     p = workloads.params("C3", seed=1)
-    ev, obs = _evolved_window(p, 20000, 12)
+    ev, obs = _evolved_window(p, 20000, 20)
     print("  C3 window events", ev, file=sys.stderr)
     assert obs[-1]["bond_num"] > 1000
     for k in ("complex", "laydown", "reject", "rl", "snap_bond"):
@@ -63,8 +63,21 @@ def test_c3_reaction_heavy_steady_state_window():
     # association x200, dissociations 1e7-1e8 x the reference): every reaction
     # and dissociation type inside the window, multi-ligand complexes
     p = workloads.params("C3", seed=2, **RATES)
-    ev, obs = _evolved_window(p, 20000, 12)
+    ev, obs = _evolved_window(p, 20000, 20)
     print("  C3-heavy window events", ev, file=sys.stderr)
     assert obs[-1]["bond_num_mono_cis"] > 0 and obs[-1]["bond_num_cis"] > 0
     for k in ("complex", "multi", "reject", "rl", "mono", "cis", "rld", "md", "cd", "snap_bond", "snap_cis"):
+        assert ev[k] > 0, k
+
+
+@pytest.mark.timeout(900)
+def test_c5_steady_state_window():
+    # C5: 1e7 particles at high ligand concentration (the reaction-heavy
+    # 1e7-particle benchmark), 10 000 steps evolved, 3-step window (the CPU
+    # oracle takes ~40 s per step at this size)
+    p = workloads.params("C5", seed=3)
+    ev, obs = _evolved_window(p, 10000, 3)
+    print("  C5 window events", ev, file=sys.stderr)
+    assert obs[-1]["bond_num"] > 100000
+    for k in ("complex", "multi", "laydown", "reject", "rl", "snap_bond"):
         assert ev[k] > 0, k

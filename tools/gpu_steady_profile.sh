@@ -41,7 +41,7 @@ if [ "$pmc" = "sq" ] || [ "$pmc" = "all" ]; then
   }
   run_pmc sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES
   run_pmc tcc TCC_HIT_sum TCC_MISS_sum
-  echo "k_bfs k_complex k_complex_heavy k_propose_free k_col_scan k_rxn_scan_tile k_rec_scatter k_rej_commit" | \
+  echo "k_bfs k_complex k_complex_heavy k_propose_free k_pair_scan k_rec_scatter k_rej_commit" | \
     python3 "$root/tools/pmc_summary.py" $(find "$out/sq" "$out/tcc" -name '*counter_collection.csv') > "$out/pmc_summary.txt"
 fi
 rm -f $state
