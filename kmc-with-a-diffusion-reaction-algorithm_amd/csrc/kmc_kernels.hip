@@ -2434,6 +2434,50 @@ __global__ void __launch_bounds__(256) k_pair_scan(KParams P, Dev d) {
     PairBuf Bc, Br;
     Bc.n = 0;
     Br.n = 0;
+#ifdef KMC_SPLIT_WALK
+    // A/B: two walks over the staged tile, each item cut to one reach
+    tile_walk(
+        P, T,
+        [&](int l, int seg, int hx, int* r0, int* r1) {
+          const int2 me = T.id[l];
+          if (me.x >= 0) return false;
+          if (me.y < 0) {
+            atomicOr(&d.ctl->err, ERR_RESOLVE);
+            return false;
+          }
+          const float4 mp = T.pos[l];
+          const bool mA = (me.x & RID_PID) < NA;
+          item_ranges(P, T, tx, ty, seg, hx, mp.x, mp.y, 0, mA ? REACH_AA : REACH_AB, r0, r1);
+          item_ranges(P, T, tx, ty, seg, hx, mp.x, mp.y, 1, mA ? REACH_AB : REACH_BB, r0 + 3, r1 + 3);
+          return true;
+        },
+        [&](int il, int nl) {
+          const int2 id = T.id[nl];
+          if (!col_pair(NA, T.id[il], T.pos[il], id, T.pos[nl])) return;
+          if (id.y < 0) atomicOr(&d.ctl->err, ERR_RESOLVE);
+          else if (Bc.n < 4) pair_push(Bc, make_int2(il, nl));
+          else col_emit(d, Lc, tile_global(T, il), tile_global(T, nl));
+        });
+    tile_walk(
+        P, T,
+        [&](int l, int seg, int hx, int* r0, int* r1) {
+          const int2 me = T.id[l];
+          if (!rxn_item(NA, me)) return false;
+          const float4 mp = T.pos[l];
+          item_ranges(P, T, tx, ty, seg, hx, mp.x, mp.y, 0, REACH_CIS, r0, r1);
+          item_ranges(P, T, tx, ty, seg, hx, mp.x, mp.y, 1, REACH_RL, r0 + 3, r1 + 3);
+          if (me.x & RID_ST3)
+            for (int k = 0; k < 3; ++k) r1[k] = r0[k];
+          if ((me.x & RID_ST2) || NB == 0)
+            for (int k = 3; k < 6; ++k) r1[k] = r0[k];
+          return true;
+        },
+        [&](int il, int nl) {
+          if (!rxn_pair(NA, T.id[il], T.pos[il], site[il], T.id[nl], T.pos[nl], site[nl])) return;
+          if (Br.n < 4) pair_push(Br, make_int2(il, nl));
+          else rxn_emit(d, Lr, tile_global(T, il), tile_global(T, nl));
+        });
+#else
     tile_walk(
         P, T,
         [&](int l, int seg, int hx, int* r0, int* r1) {
@@ -2472,6 +2516,7 @@ __global__ void __launch_bounds__(256) k_pair_scan(KParams P, Dev d) {
             else rxn_emit(d, Lr, tile_global(T, il), tile_global(T, nl));
           }
         });
+#endif
     S(d, 5);
     auto glb = [&](int2 v) { return make_int2(tile_global(T, v.x), tile_global(T, v.y)); };
     pair_flush(Bc, Lc, d.cand, &d.ctl->err, glb);

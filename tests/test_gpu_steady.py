@@ -69,15 +69,3 @@ def test_c3_reaction_heavy_steady_state_window():
     for k in ("complex", "multi", "reject", "rl", "mono", "cis", "rld", "md", "cd", "snap_bond", "snap_cis"):
         assert ev[k] > 0, k
 
-
-@pytest.mark.timeout(900)
-def test_c5_steady_state_window():
-    # C5: 1e7 particles at high ligand concentration (the reaction-heavy
-    # 1e7-particle benchmark), 10 000 steps evolved, 3-step window (the CPU
-    # oracle takes ~40 s per step at this size)
-    p = workloads.params("C5", seed=3)
-    ev, obs = _evolved_window(p, 10000, 3)
-    print("  C5 window events", ev, file=sys.stderr)
-    assert obs[-1]["bond_num"] > 100000
-    for k in ("complex", "multi", "laydown", "reject", "rl", "snap_bond"):
-        assert ev[k] > 0, k

@@ -1,0 +1,53 @@
+"""C5 steady-state window against the keyed oracle (evidence run, not part of
+the GPU test suite: the CPU oracle takes ~40 s per step at 1e7 particles).
+
+The GPU evolves C5 (1e7 particles, reference physics) for EVOLVE steps, the
+exact state it reached is handed to the cell-list oracle, and WINDOW more
+steps are compared bit for bit (every bond.dat record, full-state hash) —
+tests/test_gpu_steady.py's procedure at the largest benchmark size.
+  python -u tools/c5_window.py [evolve] [window]
+"""
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+from _kmc import O, engine, workloads  # noqa: E402
+
+
+def main():
+    evolve = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
+    window = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    p = workloads.params("C5", seed=3)
+    sim = engine.Simulation(p)
+    sim.set_state(engine.host_init_random(p))
+    t = time.time()
+    done = 0
+    while done < evolve:
+        k = min(2000, evolve - done)
+        ob = sim.step(k)
+        done += k
+        print(f"evolved {done}/{evolve}: bond_num {int(ob[-1]['bond_num'])} ({time.time() - t:.0f}s)", flush=True)
+    st = sim.get_state()
+    obs = sim.step(window)
+    h = engine.state_hash(p, sim.get_state())
+    sim.close()
+    o = O.Oracle(p, nbmode=O.NB_CELLS)
+    o.set_state(st)
+    print(f"oracle loaded ({time.time() - t:.0f}s)", flush=True)
+    ok = True
+    for s in range(window):
+        obs_o, _ = o.step(1, want_hashes=False)
+        same = obs[s] == obs_o[0]
+        ok &= bool(same)
+        print(f"step {evolve + s + 1}: {'equal' if same else 'DIFFERENT'} bond.dat record "
+              f"(bond_num {int(obs[s]['bond_num'])}) ({time.time() - t:.0f}s)", flush=True)
+    hs = o.hash()
+    print(f"state hash gpu {h:x} oracle {hs:x}: {'equal' if h == hs else 'DIFFERENT'}", flush=True)
+    print("window events", o.stats(), flush=True)
+    sys.exit(0 if ok and h == hs else 1)
+
+
+if __name__ == "__main__":
+    main()
