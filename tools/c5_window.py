@@ -12,7 +12,9 @@ import sys
 import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tests"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))  # oracle/oracle.py, as tests/conftest.py does
 from _kmc import O, engine, workloads  # noqa: E402
 
 
