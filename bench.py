@@ -76,7 +76,7 @@ TRAFFIC_JSON = "profiles/traffic_C3.json"
 
 # the proposal phase the engine brackets as "k_propose" (kmc_engine.hip
 # launch_step): these kernels back to back on the engine's stream
-PROPOSE_PHASE = ("k_bfs", "k_cx_params", "k_propose_free", "k_move_members", "k_cx_check", "k_complex_heavy")
+PROPOSE_PHASE = ("k_bfs", "k_propose_free", "k_move_members", "k_cx_check", "k_complex_heavy")
 
 
 def pmc_traffic(kernel: str, workload: str):

@@ -19,13 +19,13 @@ using namespace kmcd;
 
 // kernel ids for per-kernel HIP-event timing (kmc_set_timing / kmc_kernel_times)
 enum KId {
-  KI_CLASSIFY, KI_BFS, KI_PROPOSE, KI_PROPOSE_FREE, KI_MOVE_MEMBERS, KI_COMPLEX, KI_CX_CHECK, KI_CX_HEAVY, KI_CX_KILL, KI_SCAN,
+  KI_CLASSIFY, KI_BFS, KI_PROPOSE, KI_PROPOSE_FREE, KI_MOVE_MEMBERS, KI_CX_CHECK, KI_CX_HEAVY, KI_CX_KILL, KI_SCAN,
   KI_REC_SCATTER,
   KI_PAIR_SCAN, KI_COL_EXACT, KI_COL_ROUNDS, KI_COMMIT, KI_RXN_EXACT, KI_MATCH, KI_DISS_OBSERVE,
   KI_RESORT, KI_N
 };
 static const char* const KNAMES[KI_N] = {
-    "k_classify", "k_bfs", "k_propose", "k_propose_free", "k_move_members", "k_cx_params", "k_cx_check", "k_complex_heavy",
+    "k_classify", "k_bfs", "k_propose", "k_propose_free", "k_move_members", "k_cx_check", "k_complex_heavy",
     "k_cx_kill", "k_scan",
     "k_rec_scatter", "k_pair_scan", "k_col_exact", "k_col_rounds", "k_commit", "k_rxn_exact",
     "k_match", "k_diss_observe", "slot_resort"};
@@ -718,9 +718,10 @@ static int launch_step(kmc_sim* s, bool re_sort) {
   TIMED(KI_CLASSIFY, (k_classify<<<gN, T, 0, st>>>(K, d)));
   // KI_PROPOSE brackets the whole proposal phase: every protein's R read and
   // R_new written once (the bench's roofline unit).  Complexes kept or newly
-  // registered (k_bfs); their rigid-move parameters (k_cx_params); every unit
-  // moved by coalesced thread-per-slot streams: free receptors, cis dimers,
-  // free ligands (k_propose_free), members of complexes of <= CXL proteins
+  // registered (k_bfs); their rigid-move parameters (cx_params, in the first
+  // workgroups of k_propose_free); every unit moved by coalesced
+  // thread-per-slot streams: free receptors, cis dimers, free ligands
+  // (k_propose_free), members of complexes of <= CXL proteins
   // (k_move_members, with their complex's parameters); the complexes' lay-down / alignment tests and new
   // records (k_cx_check); the few complexes whose tests fail, with several
   // ligands or many members (k_complex_heavy).
@@ -729,9 +730,9 @@ static int launch_step(kmc_sim* s, bool re_sort) {
     const int gL = std::min(2048, (K.NB + T - 1) / T);  // grid-stride over the descriptor list
     if (K.NB > 0) {
       TIMED(KI_BFS, (k_bfs<<<gB, T, 0, st>>>(K, d)));
-      TIMED(KI_COMPLEX, (k_cx_params<<<gL, T, 0, st>>>(K, d)));
     }
-    TIMED(KI_PROPOSE_FREE, (k_propose_free<<<gN, T, 0, st>>>(K, d)));
+    const int gC = K.NB > 0 ? std::min(gL, 512) : 0;  // grid-stride over the descriptor list
+    TIMED(KI_PROPOSE_FREE, (k_propose_free<<<gC + gN, T, 0, st>>>(K, d, gC)));
     if (K.NB > 0) {
       TIMED(KI_MOVE_MEMBERS, (k_move_members<<<gN, T, 0, st>>>(K, d)));
       TIMED(KI_CX_CHECK, (k_cx_check<<<gL, T, 0, st>>>(K, d)));

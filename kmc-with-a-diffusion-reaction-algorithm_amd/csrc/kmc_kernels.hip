@@ -34,7 +34,7 @@ namespace kmcd {
 // word sustains only ≈90 atomics/µs (MI355X_MICROARCH.md, dequeue / fan-in),
 // so thousands of workgroups appending to one counter would serialise.
 #ifndef NSHARD  // counter shards per list, a power of two <= 64 (sl_prefix scans them in one wave)
-#define NSHARD 32
+#define NSHARD 64
 #endif
 struct SList {
   int2* data;
@@ -58,7 +58,7 @@ struct Dev {
   int32_t* members;  // [mcap] BFS rows of the registered complexes (kept across steps, BFS order)
   int32_t* shuf;     // [mcap] the rows after this step's multi-ligand shuffles (cluster.log)
   int4* mrec;        // [mcap] member records of rows of <= CXL members (register_complex)
-  double* cxp;       // [NB][16] rigid-move parameters of the complex rooted at lb (k_cx_params)
+  double* cxp;       // [NB][16] rigid-move parameters of the complex rooted at lb (cx_params)
   uint32_t* shuf_tag;  // [NB] step whose shuffled row of root lb is in shuf
   uint32_t mcap;     // members[] capacity (3N): rows are appended until a full rebuild
   int32_t* croot;    // [N] slot of the root ligand of the protein's registered complex, -1 none
@@ -1384,7 +1384,8 @@ __device__ __forceinline__ void cx_rigid(const KParams& P, const Dev& d, CxLds* 
 // The rigid move of a complex of at most CXL members (main.cpp:974-1131) in
 // three steps, so that its members' beads are moved by the same coalesced,
 // one-thread-per-slot stream as the free units:
-//   k_cx_params    one thread per complex: the keyed draws, the periodic shift
+//   cx_params      one thread per complex (the first workgroups of k_propose_free):
+//                  the keyed draws, the periodic shift
 //                  and the centre of mass (sums over the members' [1][1] and
 //                  [j][1] beads in BFS member order, 994-1067), the rotation
 //                  matrix -> cxp[root] (16 doubles)
@@ -1401,9 +1402,10 @@ __device__ __forceinline__ bool cx_current(const Dev& d, int4 desc) {
   return d.cx_alive[desc.x] == 1u && d.cx_off[desc.x] == desc.y;
 }
 
-__global__ void __launch_bounds__(256) k_cx_params(KParams P, Dev d) {
+// complexes c = first, first + stride, ... of the descriptor list
+__device__ __forceinline__ void cx_params(const KParams& P, const Dev& d, uint32_t first, uint32_t stride) {
   const uint32_t n = d.ctl->n_cx, step = d.ctl->step;
-  for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x) {
+  for (uint32_t c = first; c < n; c += stride) {
     const int4 desc = d.cx_list[c];
     if (!cx_current(d, desc)) continue;
     const int csize = desc.z & 0xffff, nB = desc.z >> 16, nA = csize - nB;
@@ -1662,7 +1664,7 @@ __device__ __forceinline__ void propose_one(const KParams& P, const Dev& d, int 
   }
 }
 
-// member p of a complex of at most CXL members (k_cx_params), one thread per
+// member p of a complex of at most CXL members (cx_params), one thread per
 // slot: a separate launch keeps the free units' kernel at 4 waves/SIMD
 __global__ void __launch_bounds__(256) k_move_members(KParams P, Dev d) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x, NA = P.NA;
@@ -1675,8 +1677,15 @@ __global__ void __launch_bounds__(256) k_move_members(KParams P, Dev d) {
 }
 
 // the free units, one thread per slot
-__global__ void __launch_bounds__(256) k_propose_free(KParams P, Dev d) {
-  propose_one(P, d, (int)(blockIdx.x * blockDim.x + threadIdx.x));
+// The complexes' rigid-move parameters (cx_params) run in the first gC
+// workgroups, ahead of the free units: their short dependent chains of loads
+// overlap the free units' HBM stream instead of taking a launch of their own.
+__global__ void __launch_bounds__(256) k_propose_free(KParams P, Dev d, int gC) {
+  if ((int)blockIdx.x < gC) {
+    cx_params(P, d, blockIdx.x * blockDim.x + threadIdx.x, (uint32_t)gC * blockDim.x);
+    return;
+  }
+  propose_one(P, d, (int)((blockIdx.x - gC) * blockDim.x + threadIdx.x));
 }
 
 #define RID_PID 0x00ffffff
@@ -1766,39 +1775,63 @@ __device__ __forceinline__ void load_own(const KParams& P, const Beads& B, int m
   o.z[3] = z34.y;
 }
 
+// Every coordinate of q the test needs is loaded before the first
+// comparison (one round of loads per candidate, not one per subunit); the
+// outcome is the OR of the same comparisons as the reference's loops.
 __device__ bool exact_collide(const KParams& P, const Own& o, const Beads& B, int q) {
   const int NA = P.NA;
-  if (o.isA) {
-    if (q < NA) {
-      double dx = B.A(q, 1, 1, 0) - o.x[0], dy = B.A(q, 1, 1, 1) - o.y[0], dz = B.A(q, 1, 1, 2) - o.z[0];
-      return d2(dx, dy, dz) < P.T_aa;
-    }
-    int b = q - NA;
-    for (int j = 2; j <= 4; ++j) {
-      double qx = B.B(b, j, 1, 0), qy = B.B(b, j, 1, 1), qz = B.B(b, j, 1, 2);
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (d2(qx - o.x[k], qy - o.y[k], qz - o.z[k]) < P.T_ab) return true;
-    }
-    return false;
+  const bool qA = q < NA;
+  if (o.isA && qA) {  // domain [1][1] against domain [1][1]
+    const double2 xy = B.Axy(q, 1, 1), z12 = B.A2(q, 16);
+    const double dx = xy.x - o.x[0], dy = xy.y - o.y[0], dz = z12.x - o.z[0];
+    return d2(dx, dy, dz) < P.T_aa;
   }
-  if (q >= NA) {
-    int b = q - NA;
-    for (int j = 2; j <= 4; ++j) {
-      double qx = B.B(b, j, 1, 0), qy = B.B(b, j, 1, 1), qz = B.B(b, j, 1, 2);
+  // [j][1] beads of q, j = 1..4: (x, y) rows and the two z rows
+  double qx[4], qy[4], qz[4];
+  double2 z12, z34;
+  if (qA) {
 #pragma unroll
-      for (int k = 1; k < 4; ++k)
-        if (d2(qx - o.x[k], qy - o.y[k], qz - o.z[k]) < P.T_bb) return true;
+    for (int j = 0; j < 4; ++j) {
+      const double2 xy = B.Axy(q, j + 1, 1);
+      qx[j] = xy.x;
+      qy[j] = xy.y;
     }
-    return false;
-  }
-  for (int j = 1; j <= 4; ++j) {
-    double qx = B.A(q, j, 1, 0), qy = B.A(q, j, 1, 1), qz = B.A(q, j, 1, 2);
+    z12 = B.A2(q, 16);
+    z34 = B.A2(q, 20);
+  } else {
+    const int b = q - NA;
+    qx[0] = qy[0] = 0.0;
 #pragma unroll
-    for (int k = 1; k < 4; ++k)
-      if (d2(qx - o.x[k], qy - o.y[k], qz - o.z[k]) < P.T_ab) return true;
+    for (int j = 1; j < 4; ++j) {
+      const double2 xy = B.Bxy(b, j + 1, 1);
+      qx[j] = xy.x;
+      qy[j] = xy.y;
+    }
+    z12 = B.B2(b, 8);
+    z34 = B.B2(b, 10);
   }
-  return false;
+  qz[0] = z12.x;
+  qz[1] = z12.y;
+  qz[2] = z34.x;
+  qz[3] = z34.y;
+  bool hit = false;
+  if (o.isA) {  // receptor domains k = 1..4 against ligand subunits j = 2..4
+#pragma unroll
+    for (int j = 1; j < 4; ++j)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) hit |= d2(qx[j] - o.x[k], qy[j] - o.y[k], qz[j] - o.z[k]) < P.T_ab;
+  } else if (!qA) {  // ligand subunits against ligand subunits
+#pragma unroll
+    for (int j = 1; j < 4; ++j)
+#pragma unroll
+      for (int k = 1; k < 4; ++k) hit |= d2(qx[j] - o.x[k], qy[j] - o.y[k], qz[j] - o.z[k]) < P.T_bb;
+  } else {  // ligand subunits against receptor domains j = 1..4
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int k = 1; k < 4; ++k) hit |= d2(qx[j] - o.x[k], qy[j] - o.y[k], qz[j] - o.z[k]) < P.T_ab;
+  }
+  return hit;
 }
 
 // conservative single-precision prefilter on reference points (margins ≥ 1 Å
@@ -2434,50 +2467,6 @@ __global__ void __launch_bounds__(256) k_pair_scan(KParams P, Dev d) {
     PairBuf Bc, Br;
     Bc.n = 0;
     Br.n = 0;
-#ifdef KMC_SPLIT_WALK
-    // A/B: two walks over the staged tile, each item cut to one reach
-    tile_walk(
-        P, T,
-        [&](int l, int seg, int hx, int* r0, int* r1) {
-          const int2 me = T.id[l];
-          if (me.x >= 0) return false;
-          if (me.y < 0) {
-            atomicOr(&d.ctl->err, ERR_RESOLVE);
-            return false;
-          }
-          const float4 mp = T.pos[l];
-          const bool mA = (me.x & RID_PID) < NA;
-          item_ranges(P, T, tx, ty, seg, hx, mp.x, mp.y, 0, mA ? REACH_AA : REACH_AB, r0, r1);
-          item_ranges(P, T, tx, ty, seg, hx, mp.x, mp.y, 1, mA ? REACH_AB : REACH_BB, r0 + 3, r1 + 3);
-          return true;
-        },
-        [&](int il, int nl) {
-          const int2 id = T.id[nl];
-          if (!col_pair(NA, T.id[il], T.pos[il], id, T.pos[nl])) return;
-          if (id.y < 0) atomicOr(&d.ctl->err, ERR_RESOLVE);
-          else if (Bc.n < 4) pair_push(Bc, make_int2(il, nl));
-          else col_emit(d, Lc, tile_global(T, il), tile_global(T, nl));
-        });
-    tile_walk(
-        P, T,
-        [&](int l, int seg, int hx, int* r0, int* r1) {
-          const int2 me = T.id[l];
-          if (!rxn_item(NA, me)) return false;
-          const float4 mp = T.pos[l];
-          item_ranges(P, T, tx, ty, seg, hx, mp.x, mp.y, 0, REACH_CIS, r0, r1);
-          item_ranges(P, T, tx, ty, seg, hx, mp.x, mp.y, 1, REACH_RL, r0 + 3, r1 + 3);
-          if (me.x & RID_ST3)
-            for (int k = 0; k < 3; ++k) r1[k] = r0[k];
-          if ((me.x & RID_ST2) || NB == 0)
-            for (int k = 3; k < 6; ++k) r1[k] = r0[k];
-          return true;
-        },
-        [&](int il, int nl) {
-          if (!rxn_pair(NA, T.id[il], T.pos[il], site[il], T.id[nl], T.pos[nl], site[nl])) return;
-          if (Br.n < 4) pair_push(Br, make_int2(il, nl));
-          else rxn_emit(d, Lr, tile_global(T, il), tile_global(T, nl));
-        });
-#else
     tile_walk(
         P, T,
         [&](int l, int seg, int hx, int* r0, int* r1) {
@@ -2516,7 +2505,6 @@ __global__ void __launch_bounds__(256) k_pair_scan(KParams P, Dev d) {
             else rxn_emit(d, Lr, tile_global(T, il), tile_global(T, nl));
           }
         });
-#endif
     S(d, 5);
     auto glb = [&](int2 v) { return make_int2(tile_global(T, v.x), tile_global(T, v.y)); };
     pair_flush(Bc, Lc, d.cand, &d.ctl->err, glb);

@@ -47,8 +47,14 @@ def _oracle_outputs(p, o, steps, out, tmp):
     return "".join(lines), cpt.read_bytes(), gro.read_bytes(), clu.read_bytes()
 
 
+def _require_built():
+    # GPU tests never compile: a stale build would be silently replaced
+    # mid-suite (build in-tree first: __graft_entry__.build())
+    assert not build.stale(), "libkmc.so / kmc_run are older than their sources: run __graft_entry__.build()"
+
+
 def test_kmc_run_fresh_and_resume(tmp_path):
-    build.build()
+    _require_built()
     p = params(seed=17, **DENSE)
     wd = tmp_path / "run"
     wd.mkdir()
@@ -82,7 +88,7 @@ def test_kmc_run_exact_state_resume(tmp_path):
     # one 2000-step run vs 1000 + 1000 steps resumed from the exact state
     # file: the final state files are byte-identical (position.cpt alone
     # cannot give this, main.cpp:2208-2209)
-    build.build()
+    _require_built()
     p = params(seed=19, **DENSE)
     one, two = tmp_path / "one", tmp_path / "two"
     one.mkdir()
