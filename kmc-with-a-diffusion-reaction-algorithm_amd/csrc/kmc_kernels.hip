@@ -2715,18 +2715,64 @@ struct CisV {
   }
 };
 
+// Few edges (the common case: tens per step at the benchmark sizes): wave 0
+// sorts the keys in registers (bitonic network over the 64 lanes, written back
+// in order to keys[0..n)) and lane 0 takes them greedily in that order — the
+// definition of the lexicographic-first matching — instead of the sort and
+// dependency rounds of block_greedy, whose barriers dominate at this size.
+#define SMALL_EDGES 64
+template <typename VF>
+__device__ void small_greedy(uint32_t n, uint64_t* keys, VF vtx, uint8_t* acc) {
+  __shared__ uint64_t sk[64];
+  __shared__ uint32_t taken[2 * SMALL_EDGES];
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    uint64_t k = lane < (int)n ? keys[lane] : ~0ull;
+#pragma unroll
+    for (int size = 2; size <= 64; size <<= 1)
+#pragma unroll
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        const uint64_t o = (uint64_t)__shfl_xor((long long)k, stride, 64);
+        const bool asc = (lane & size) == 0, low = (lane & stride) == 0;
+        k = (low == asc) ? (k < o ? k : o) : (k < o ? o : k);
+      }
+    if (lane < (int)n) keys[lane] = k;
+    sk[lane] = k;
+    wave_sync();
+    if (lane == 0) {
+      uint32_t nt = 0;
+      for (uint32_t e = 0; e < n; ++e) {
+        const uint64_t ke = sk[e];
+        const uint32_t a = vtx(ke, 0), b = vtx(ke, 1);
+        bool free = true;
+        for (uint32_t t = 0; t < nt; ++t) free &= taken[t] != a && taken[t] != b;
+        acc[e] = free ? 1 : 0;
+        if (free) {
+          taken[nt++] = a;
+          taken[nt++] = b;
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
+
 // R–L association, main.cpp:1877-1949
 __device__ void rl_match(const KParams& P, const Dev& d) {
   const int NA = P.NA, NB = P.NB;
   uint32_t n = d.ctl->n_rl;
   if (n == 0) return;
   if (n > d.cap_edges) n = d.cap_edges;
-  uint32_t np = pow2ceil(n);
-  for (uint32_t e = n + threadIdx.x; e < np; e += blockDim.x) d.rl_keys[e] = ~0ull;
-  __syncthreads();
-  block_sort(d.rl_keys, np);
   uint8_t* acc = (uint8_t*)(d.gi32 + 5 * d.cap_edges);
-  block_greedy(n, d.rl_keys, RLV{P.N}, d.ent, d.gi32, acc, &d.ctl->err);
+  if (n <= SMALL_EDGES) {
+    small_greedy(n, d.rl_keys, RLV{P.N}, acc);
+  } else {
+    uint32_t np = pow2ceil(n);
+    for (uint32_t e = n + threadIdx.x; e < np; e += blockDim.x) d.rl_keys[e] = ~0ull;
+    __syncthreads();
+    block_sort(d.rl_keys, np);
+    block_greedy(n, d.rl_keys, RLV{P.N}, d.ent, d.gi32, acc, &d.ctl->err);
+  }
   for (uint32_t e = threadIdx.x; e < n; e += blockDim.x) {
     if (!acc[e]) continue;
     uint64_t key = d.rl_keys[e];
@@ -2767,11 +2813,15 @@ __device__ void cis_match(const KParams& P, const Dev& d) {
     __syncthreads();
     uint32_t n = m;
     if (n > 0) {
-      uint32_t np = pow2ceil(n);
-      for (uint32_t t = n + threadIdx.x; t < np; t += blockDim.x) e[t] = ~0ull;
-      __syncthreads();
-      block_sort(e, np);
-      block_greedy(n, e, CisV{}, d.ent, d.gi32, acc, &d.ctl->err);
+      if (n <= SMALL_EDGES) {
+        small_greedy(n, e, CisV{}, acc);
+      } else {
+        uint32_t np = pow2ceil(n);
+        for (uint32_t t = n + threadIdx.x; t < np; t += blockDim.x) e[t] = ~0ull;
+        __syncthreads();
+        block_sort(e, np);
+        block_greedy(n, e, CisV{}, d.ent, d.gi32, acc, &d.ctl->err);
+      }
       for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) {
         if (!acc[t]) continue;
         int i = d.slot_of[(int)(e[t] >> 34)], q = d.slot_of[(int)((e[t] >> 2) & 0xffffffffu)];
