@@ -2717,14 +2717,14 @@ struct CisV {
 
 // Few edges (the common case: tens per step at the benchmark sizes): wave 0
 // sorts the keys in registers (bitonic network over the 64 lanes, written back
-// in order to keys[0..n)) and lane 0 takes them greedily in that order — the
-// definition of the lexicographic-first matching — instead of the sort and
-// dependency rounds of block_greedy, whose barriers dominate at this size.
+// in order to keys[0..n)); lane l then holds sorted edge l's two vertices, and
+// the wave takes the edges in that order — the definition of the
+// lexicographic-first matching — each decided by one ballot against the
+// edges accepted before it, instead of the sort and dependency rounds of
+// block_greedy, whose barriers dominate at this size.
 #define SMALL_EDGES 64
 template <typename VF>
 __device__ void small_greedy(uint32_t n, uint64_t* keys, VF vtx, uint8_t* acc) {
-  __shared__ uint64_t sk[64];
-  __shared__ uint32_t taken[2 * SMALL_EDGES];
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     uint64_t k = lane < (int)n ? keys[lane] : ~0ull;
@@ -2736,23 +2736,16 @@ __device__ void small_greedy(uint32_t n, uint64_t* keys, VF vtx, uint8_t* acc) {
         const bool asc = (lane & size) == 0, low = (lane & stride) == 0;
         k = (low == asc) ? (k < o ? k : o) : (k < o ? o : k);
       }
-    if (lane < (int)n) keys[lane] = k;
-    sk[lane] = k;
-    wave_sync();
-    if (lane == 0) {
-      uint32_t nt = 0;
-      for (uint32_t e = 0; e < n; ++e) {
-        const uint64_t ke = sk[e];
-        const uint32_t a = vtx(ke, 0), b = vtx(ke, 1);
-        bool free = true;
-        for (uint32_t t = 0; t < nt; ++t) free &= taken[t] != a && taken[t] != b;
-        acc[e] = free ? 1 : 0;
-        if (free) {
-          taken[nt++] = a;
-          taken[nt++] = b;
-        }
-      }
+    const bool real = lane < (int)n;
+    if (real) keys[lane] = k;
+    const uint32_t va = real ? vtx(k, 0) : 0xffffffffu, vb = real ? vtx(k, 1) : 0xffffffffu;
+    uint64_t accm = 0;  // accepted edges so far (bits < e)
+    for (uint32_t e = 0; e < n; ++e) {
+      const uint32_t a = (uint32_t)__shfl((int)va, (int)e, 64), b = (uint32_t)__shfl((int)vb, (int)e, 64);
+      const bool shares = (va == a) | (va == b) | (vb == a) | (vb == b);
+      if ((__ballot(shares) & accm) == 0) accm |= 1ull << e;
     }
+    if (real) acc[lane] = (uint8_t)((accm >> lane) & 1ull);
   }
   __syncthreads();
 }
