@@ -67,8 +67,8 @@ struct Dev {
   int32_t* dlist;    // [2][N] proteins whose bonds changed during step s (list s & 1)
   uint32_t* pend;    // [N] round tag: unit still waiting (resolution pass C)
   int32_t* overflow; // [NB]
-  int4* cx_list;     // [NB] descriptors of this step's complexes of <= CXL members (k_complex)
-  int4* cx_heavy;    // [NB] descriptors for k_complex_heavy: larger complexes, and those k_complex
+  int4* cx_list;     // [NB] descriptors of the registered complexes (kept across steps; cx_params, k_cx_check)
+  int4* cx_heavy;    // [NB] descriptors for k_complex_heavy: larger complexes, and those k_cx_check
                      //      moved but whose lay-down / alignment changes beads
   int32_t* cell_cnt;    // [ncell+1] this step's record counts (counted by the proposals, read by the scan)
   int32_t* cell_cnt_alt;  // [ncell+1] the next step's counts: zeroed by k_diss_observe, swapped after the step
@@ -141,7 +141,7 @@ __device__ __forceinline__ int cell_y(const KParams& P, double y) {
   return c < 0 ? 0 : (c >= P.ncy ? P.ncy - 1 : c);
 }
 
-#define CXL 16  // members of a complex staged in LDS by k_complex (see §complexes)
+#define CXL 16  // members of a complex moved by the streamed path and staged in LDS by k_complex_heavy
 
 // slot for each calling lane (call from the lanes that emit)
 __device__ __forceinline__ uint32_t wave_slot(uint32_t* ctr) {
@@ -286,14 +286,14 @@ __device__ __forceinline__ void nbrs3(const KParams& P, const Dev& d, int x, int
 }
 
 // Complex descriptor (cx_list / cx_heavy): x = root ligand lb | CXD_MOVED
-// (rigid move already done by k_complex), y = members[] offset, z = size |
+// (rigid move already done by k_move_members), y = members[] offset, z = size |
 // ligands << 16, w = the root's reference index (its random-stream key).
 #define CXD_MOVED (1 << 30)
 #define CXD_LB 0x3fffffff
 
 // Register the component in queue q (q[t * STRIDE], t < qn, BFS order) rooted
-// at ligand slot p: member row, owner keys, descriptor on cx_list (k_complex
-// stages complexes of at most CXL members in LDS and hands larger ones to the
+// at ligand slot p: member row, owner keys, descriptor on cx_list (complexes
+// of at most CXL members take the streamed path, larger ones the
 // global-memory path of k_complex_heavy).
 template <int STRIDE = 1>
 __device__ __forceinline__ void register_complex(const KParams& P, const Dev& d, int p, const int* q, int qn) {
@@ -360,7 +360,7 @@ __device__ __forceinline__ void register_complex(const KParams& P, const Dev& d,
   d.cx_nb[b] = nb;
   d.ukind[p] = U_COMPLEX;
   // the descriptor list is kept across steps too: a descriptor is current
-  // while its root is alive with the same row offset (k_complex checks)
+  // while its root is alive with the same row offset (cx_current checks)
   const int4 desc = make_int4(b, (int)off, qn | nb << 16, rootid);
   const uint32_t slot = wave_slot(&d.ctl->n_cx);
   if (slot < d.mcap / 2) d.cx_list[slot] = desc;
@@ -441,7 +441,7 @@ __global__ void __launch_bounds__(256) k_bfs(KParams P, Dev d) {
 
 // Component of overflow entry o (larger than BFS_QCAP): one thread, global
 // queue + visit tags.  Returns the root's ligand index if it roots the
-// component (registered, unlisted), else -1.  Called by k_complex.
+// component (registered, unlisted), else -1.  Called by k_complex_heavy.
 __device__ __forceinline__ int bfs_overflow_one(const KParams& P, const Dev& d, uint32_t o) {
   const int NA = P.NA;
   int p = NA + d.overflow[o];
@@ -530,7 +530,8 @@ __device__ __forceinline__ int rec_cell(const KParams& P, double x, double y, in
 
 
 // A protein's two records (old and proposed position) are counted into their
-// cells by the thread that wrote the proposal (k_propose / k_complex); the
+// cells by the thread that wrote the proposal (k_propose_free / k_cx_check /
+// k_complex_heavy); the
 // rank within the cell is kept for the scatter.
 __device__ __forceinline__ void count_records(const KParams& P, const Dev& d, int p) {
   double x, y, zl, zh;
@@ -855,7 +856,9 @@ struct Stamper {
 // ---------------------------------------------------------------- complexes
 // Ligand-rooted complex of size > 1: rigid move (main.cpp:974-1131), lay-down
 // of a single ligand (1138-1193), receptor / cis re-alignment (1196-1274),
-// multi-ligand alignment (1284-1732) — one wave per complex (k_complex).
+// multi-ligand alignment (1284-1732).  The common case is streamed (below:
+// cx_params, k_move_members, k_cx_check); the rest runs one wave per complex
+// (k_complex_heavy).
 //
 // A complex of up to CXL members is staged in LDS: the wave loads the member
 // slots and links, moves the beads (lanes over (member, bead)) into LDS, lane
@@ -1567,7 +1570,7 @@ __global__ void __launch_bounds__(256) k_cx_check(KParams P, Dev d) {
 // runs the lay-down / alignment code against LDS; larger ones run the rigid
 // move and the alignment on global memory.  Block 0's first wave first runs
 // the BFS of the components that overflowed k_bfs's LDS queue (> BFS_QCAP
-// members) and moves those it roots.  Launched after k_complex on its stream.
+// members) and moves those it roots.  Launched after k_cx_check on its stream.
 __global__ void __launch_bounds__(256) k_complex_heavy(KParams P, Dev d) {
   __shared__ CxLds lds[4];
   const int lane = __lane_id(), NA = P.NA, NB = P.NB;
@@ -1641,7 +1644,7 @@ __global__ void __launch_bounds__(256) k_complex_heavy(KParams P, Dev d) {
     wave_sync();
     cx_write_back(d, L, d.shuf + desc.y, csize, nB, NA, lane);  // shuffled row: shuf (members keeps BFS order)
     if (nB > 1 && lane == 0) d.shuf_tag[lb] = step;
-    cx_count(P, d, L, csize, lane, lane < csize ? d.rank[L->slot[lane]].x : 0);  // old rank: k_complex
+    cx_count(P, d, L, csize, lane, lane < csize ? d.rank[L->slot[lane]].x : 0);  // old rank: k_move_members
     wave_sync();
   }
 }
