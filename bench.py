@@ -208,11 +208,17 @@ def run_rank(args, rank: int, world: int, local: int):
     # a diagnostic library (KMC_DIAG=1 KMC_LIB_PATH=..., capi.py) is named in the line
     library = os.path.relpath(engine.load_library()._name, REPO)
 
-    if world > 1:
-        torch.cuda.set_device(local)
+    # RCCL (backend "nccl") at every world size: at N = 1 the ensemble
+    # reduction below runs the same device-tensor all-reduce path as on 8 GPUs
+    torch.cuda.set_device(local)
+    if world == 1 and "MASTER_ADDR" not in os.environ:
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                                device_id=torch.device("cuda", local))
+    else:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        if dist.get_world_size() != world:
-            sys.exit(f"bench.py: process group has {dist.get_world_size()} ranks, expected {world}")
+    if dist.get_world_size() != world:
+        sys.exit(f"bench.py: process group has {dist.get_world_size()} ranks, expected {world}")
+    if world > 1:
         props = torch.cuda.get_device_properties(local)
         me = str(getattr(props, "uuid", "")) or f"{props.name}:{local}"
         devs = [None] * world
@@ -240,12 +246,15 @@ def run_rank(args, rank: int, world: int, local: int):
             dist.barrier()
         torch.cuda.synchronize(dev)
 
+    last_obs = {}
+
     def timed(k):
         barrier()
         t = time.perf_counter()
         obs = sim.step(k)
         red = ensemble.reduce(obs, device=dev)
         barrier()
+        last_obs["obs"] = obs
         return time.perf_counter() - t, red
 
     def max_over_ranks(x):
@@ -289,6 +298,14 @@ def run_rank(args, rank: int, world: int, local: int):
     sim.set_timing([dom], every=TIMING_EVERY)
     dt_local, (sums, maxima, cluster) = timed(args.steps)
     dt, per_rank = max_over_ranks(dt_local)
+
+    # what the all-reduce did: at N = 1 the reduced series must equal this
+    # rank's own observables (the same RCCL call the N-GPU run makes)
+    own_s, own_m = ensemble.pack(last_obs["obs"])
+    reduce_info = {"backend": dist.get_backend(), "device": str(dev), "world": world,
+                   "ops": ["all_reduce SUM int64[K,6]", "all_reduce MAX int64[K,1]"], "steps_reduced": args.steps}
+    if world == 1:
+        reduce_info["equals_local"] = bool((sums == own_s).all() and (maxima == own_m).all())
 
     total_ms, launches = sim.kernel_times().get(dom, (0.0, 0))
     avg_s = total_ms / 1e3 / max(launches, 1)
@@ -356,12 +373,12 @@ def run_rank(args, rank: int, world: int, local: int):
                 "step_frac": step_b / (ms_per_step / 1e3) / 1e9 / HBM_PEAK_GBS,
             },
             "cpu_baseline": cpu,
+            "ensemble_reduce": reduce_info,
             "library": library,
         }
         print(json.dumps(line), flush=True)
     sim.close()
-    if world > 1:
-        dist.destroy_process_group()
+    dist.destroy_process_group()
 
 
 # ---------------------------------------------------------------- CPU baseline

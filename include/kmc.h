@@ -157,7 +157,10 @@ const char* kmc_kernel_name(int32_t id);
 /* BFS member rows of the last simulated step (results[i][.] of main.cpp:537,
  * after the multi-ligand shuffles): for each ligand b, row_len[b] members
  * (reference 1-based indices) are appended to `members` (n_a+n_b capacity);
- * non-root ligands have row_len 0.  Feeds cluster.log (main.cpp:2291-2305). */
+ * non-root ligands have row_len 0.  Feeds cluster.log (main.cpp:2291-2305).
+ * KMC_ERR_ARG before the first step after a state was set, and after a
+ * kmc_step that failed without keeping a step (the rows would not describe
+ * the current state). */
 int kmc_get_clusters(kmc_sim* s, int32_t* row_len, int32_t* members);
 
 /* Formatting helpers shared by every host driver.  Each returns the number of

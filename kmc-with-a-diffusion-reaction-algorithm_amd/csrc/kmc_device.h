@@ -39,6 +39,7 @@ struct Ctl {
   uint32_t obs_idx;       // record index within the current kmc_step call
   uint32_t err;           // error bits (ERR_*)
   uint32_t err_step;      // first step whose kernels raised an error bit (k_finalize), 0 = none
+  uint32_t err_first;     // the error bits raised by that step (its cause; later bits may be consequences)
   // per-step work-list counters
   uint32_t n_overflow;    // ligands whose BFS overflowed the register queue
   uint32_t cx_cursor;     // members[] allocation cursor (rows are kept across steps; k_cx_kill resets)
@@ -54,7 +55,10 @@ struct Ctl {
   // observable bookkeeping (the per-step counts are reduced by k_finalize)
   int32_t off_bond, off_rl, off_cis, off_mono;  // counters − derived at load
   int32_t maxc;                                 // protein_num_in_Max_Complex
-  int32_t pad2;
+  uint32_t force_full;    // k_finalize: the next step's k_cx_kill rebuilds every complex (members[] half
+                          // full, or a dirty list overflowed); only k_finalize writes it
+  uint32_t n_forced;      // diagnostics: full complex rebuilds latched by force_full since the state was set
+  uint32_t pad3;
   uint64_t vtag;          // BFS tag counter for the overflow path
   uint64_t stamps[24];    // diagnostic build (-DKMC_STAMPS) only: phase cycles (tile scans, complexes)
 };

@@ -59,6 +59,9 @@ struct kmc_sim {
   // undone chunk); KMC_FULL_BFS=1: every step
   bool need_full = true, always_full = false;
   bool debug_counts = false;  // KMC_DEBUG_COUNTS=1: print the last step's work counts per kmc_step chunk
+  // the unit tables (ukind, complex rows) describe the current step: false
+  // after a new state and after a chunk undone without a kept step
+  bool clusters_valid = false;
   // slot order (kmc_kernels.hip §slot order): scratch of the re-sort
   int64_t resort_every = 100, since_resort = 0;
   int key_bits = 1;
@@ -488,6 +491,10 @@ static int clear_step_tags(kmc_sim* s) {
   HIPCHK(s, hipMemsetAsync(d.cell_cnt, 0, sizeof(int32_t) * (size_t)d.ncnt, st));
   HIPCHK(s, hipMemsetAsync(d.cell_cnt_alt, 0, sizeof(int32_t) * (size_t)d.ncnt, st));
   HIPCHK(s, hipMemsetAsync(d.shard_cnt, 0, sizeof(uint32_t) * 5 * NSHARD, st));
+  // BFS candidates and shuffled rows are tagged with the step: an undone
+  // chunk's tags would match the replayed steps' numbers
+  HIPCHK(s, hipMemsetAsync(d.bfs_cand, 0, sizeof(uint32_t) * (size_t)s->K.NB, st));
+  HIPCHK(s, hipMemsetAsync(d.shuf_tag, 0, sizeof(uint32_t) * (size_t)s->K.NB, st));
   return KMC_OK;
 }
 
@@ -565,9 +572,15 @@ int kmc_set_state(kmc_sim* s, const kmc_state_view* v) {
   if (rc != KMC_OK) return rc;
   HIPCHK(s, hipStreamSynchronize(s->stream));
   s->step_done = v->step;
-  s->since_resort = 0;
+  // the sort above had no unit keys (owner, croot are set by the first
+  // step): re-sort right before the second step, so that complex members
+  // are grouped after the free units from then on, not only after the first
+  // periodic re-sort (a loaded state otherwise runs its first resort_every
+  // steps in the ungrouped layout)
+  s->since_resort = s->resort_every >= 2 ? s->resort_every - 2 : 0;
   s->have_state = true;
   s->need_full = true;
+  s->clusters_valid = false;
   return KMC_OK;
 }
 
@@ -872,13 +885,16 @@ int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out) {
       if (rc != KMC_OK) return rc;
       const uint32_t err = s->ctl_host->err;
       if (!err) break;
+      // the failing step's own bits: later steps of the chunk ran on its
+      // dropped entries, so their bits may be consequences
+      const uint32_t cause = s->ctl_host->err_first;
       const int64_t bad = (int64_t)s->ctl_host->err_step;
       rc = snapshot(s, true);
       if (rc != KMC_OK) return rc;
       s->since_resort = since0;
       s->need_full = true;  // the kept complexes may describe the undone steps
       ++s->n_replays;
-      if (err == ERR_EDGES && s->grow < 6) {  // at most 64x the default lists
+      if ((cause & ERR_EDGES) && s->grow < 6) {  // at most 64x the default lists
         s->grow += 1;
         if (alloc_lists(s) != KMC_OK) return fail(s, KMC_ERR_HIP, "growing the output lists failed");
         continue;
@@ -892,20 +908,22 @@ int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out) {
           HIPCHK(s, hipMemcpy(out + done, s->obs_buf, sizeof(kmc_obs_dev) * good, hipMemcpyDeviceToHost));
         s->step_done += good;
       }
+      s->clusters_valid = good > 0;
       char m[200];
       snprintf(m, sizeof m, "device error bits 0x%x at step %lld; state kept at step %lld", err, (long long)bad,
                (long long)s->step_done);
-      const int code = (err & ERR_GEOMETRY) ? KMC_ERR_GEOMETRY : KMC_ERR_CAPACITY;
+      const int code = (cause & ERR_GEOMETRY) ? KMC_ERR_GEOMETRY : KMC_ERR_CAPACITY;
       return fail(s, code, m);
     }
     if (out)
       HIPCHK(s, hipMemcpy(out + done, s->obs_buf, sizeof(kmc_obs_dev) * n, hipMemcpyDeviceToHost));
     s->step_done += n;
+    s->clusters_valid = true;
     if (s->debug_counts) {
       const uint32_t* l = s->ctl_host->last;
-      fprintf(stderr, "kmc step %lld: candidates %u conflicts %u pending-units %u rejected %u rxn-pairs %u rl-edges %u cis-edges %u bfs-overflow %u (list growth 2^%d, replays %lld)\n",
+      fprintf(stderr, "kmc step %lld: candidates %u conflicts %u pending-units %u rejected %u rxn-pairs %u rl-edges %u cis-edges %u bfs-overflow %u (list growth 2^%d, replays %lld, forced rebuilds %u)\n",
               (long long)s->step_done, l[0], l[1], l[2], l[3], l[4], l[5], l[6], l[7], s->grow,
-              (long long)s->n_replays);
+              (long long)s->n_replays, s->ctl_host->n_forced);
       const uint64_t* t = s->ctl_host->stamps;
       if (t[16])
         fprintf(stderr, "kmc stamps cx stage %llu rigid %llu checks %llu writeback %llu count %llu next %llu\n",
@@ -963,7 +981,8 @@ int kmc_device_math(int op, const double* x, const double* y, double* out, int64
 
 int kmc_get_clusters(kmc_sim* s, int32_t* row_len, int32_t* members) {
   if (!s || !row_len || !members) return KMC_ERR_ARG;
-  if (s->step_done == 0 || !s->have_state) return fail(s, KMC_ERR_ARG, "no step simulated yet");
+  if (!s->have_state || !s->clusters_valid)
+    return fail(s, KMC_ERR_ARG, "no step simulated since the state was set (or the last chunk was undone)");
   const int NA = s->p.n_a, NB = s->p.n_b, N = NA + NB;
   std::vector<uint8_t> kind(N);
   std::vector<int32_t> off(NB), size(NB), mem(N), id_of(N), slot_of(N);

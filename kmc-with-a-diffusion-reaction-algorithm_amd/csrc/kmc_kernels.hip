@@ -223,7 +223,9 @@ __global__ void k_classify(KParams P, Dev d) {
 __global__ void k_cx_kill(KParams P, Dev d, int full) {
   const int NA = P.NA;
   const uint32_t step = d.ctl->step;
-  full |= d.ctl->cx_cursor > d.mcap / 2;
+  // latched by the previous step's k_finalize: this kernel resets cx_cursor,
+  // so it must not derive the branch from it (blocks would disagree)
+  full |= d.ctl->force_full;
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, nt = gridDim.x * blockDim.x;
   if (full) {
     for (uint32_t p = tid; p < (uint32_t)P.N; p += nt) d.croot[p] = -1;
@@ -251,12 +253,15 @@ __global__ void k_cx_kill(KParams P, Dev d, int full) {
   }
 }
 
-// a bond of protein p formed or broke this step (dirty list of step & 1)
+// a bond of protein p formed or broke this step (dirty list of step & 1).
+// Without ligands no complex exists and the list is never read.  A list that
+// overflows (a protein can be listed several times) is not an error: the
+// next step rebuilds every complex instead (k_finalize latches force_full).
 __device__ __forceinline__ void mark_bond_change(const KParams& P, const Dev& d, int p, uint32_t step) {
+  if (P.NB == 0) return;
   const uint32_t li = step & 1;
   const uint32_t t = atomicAdd(&d.ctl->n_dirty[li], 1u);
   if (t < (uint32_t)P.N) d.dlist[(size_t)li * P.N + t] = p;
-  else atomicOr(&d.ctl->err, ERR_MEMBERS);
 }
 
 // ================================================================ BFS
@@ -2995,7 +3000,15 @@ __global__ void __launch_bounds__(256) k_finalize(KParams P, Dev d, double time_
   o.tot_clu = tot_clu;
   o.reserved = 0;
   d.obs[obs_idx] = o;
-  if (c->err && c->err_step == 0) c->err_step = step;  // kmc_step replays up to here
+  if (c->err && c->err_step == 0) {  // kmc_step replays up to here
+    c->err_step = step;
+    c->err_first = c->err;
+  }
+  // the next step's k_cx_kill: rebuild every complex when the appended rows
+  // fill half of members[] or this step's dirty list overflowed
+  const uint32_t ff = (c->cx_cursor > d.mcap / 2 || c->n_dirty[step & 1] > (uint32_t)P.N) ? 1u : 0u;
+  c->force_full = ff;
+  c->n_forced += ff;
   c->maxc = maxc;
   c->obs_idx = obs_idx + 1;
   c->step = step + 1;

@@ -135,3 +135,91 @@ def test_two_gpu_replicas_reduced_equal_oracle_sum(tmp_path):
     assert np.array_equal(got["s"], sa + sb)
     assert np.array_equal(got["m"], np.maximum(ma, mb))
     assert (sa + sb)[-1, 3] > 0, "the window should form bonds"
+
+
+# ---------------------------------------------------------------- RCCL on the GPU
+def _nccl_worker(rank, world, port, out, steps):
+    import torch
+    import torch.distributed as dist
+
+    engine = importlib.import_module(PKG + ".engine")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+                            device_id=dev)
+    assert dist.get_backend() == "nccl"
+    p = params(seed=99, replica=rank, **DENSE)
+    with engine.Simulation(p, device=0) as sim:
+        sim.set_state(engine.host_init_random(p))
+        obs = sim.step(steps)
+    s, m, cluster = ensemble.reduce(obs, device=dev)  # device tensors through RCCL
+    if rank == 0:
+        np.savez(out, s=s, m=m, cluster=cluster, obs=obs)
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_rccl_one_rank_reduce_equals_oracle(tmp_path):
+    # the ensemble reduction of bench.py / C4 (main.cpp:2247-2253 observables)
+    # through RCCL on device tensors: a 1-rank "nccl" group on the GPU (RCCL
+    # refuses two ranks on one device); the reduced series equals the keyed
+    # oracle's own series of the same replica
+    engine = importlib.import_module(PKG + ".engine")
+    steps = 300
+    out = str(tmp_path / "ens_nccl.npz")
+    mp.spawn(_nccl_worker, args=(1, _free_port(), out, steps), nprocs=1, join=True)
+    got = np.load(out)
+    p = params(seed=99, replica=0, **DENSE)
+    o = O.Oracle(p)
+    o.set_state(engine.host_init_random(p))
+    ref = o.step(steps, want_hashes=False)[0]
+    assert np.array_equal(got["obs"], ref)
+    s, m = ensemble.pack(ref)
+    assert np.array_equal(got["s"], s)
+    assert np.array_equal(got["m"], m)
+    assert s[-1, 3] > 0, "the window should form bonds"
+
+
+def _c3_worker(rank, world, port, out, steps):
+    import torch.distributed as dist
+
+    engine = importlib.import_module(PKG + ".engine")
+    workloads = importlib.import_module(PKG + ".workloads")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    p = workloads.params("C3", seed=1, replica=rank)
+    with engine.Simulation(p, device=0) as sim:
+        sim.set_state(engine.host_init_random(p))
+        obs = sim.step(steps)
+    s, m, cluster = ensemble.reduce(obs)
+    np.save(out + f".obs{rank}.npy", obs)
+    if rank == 0:
+        np.savez(out, s=s, m=m, cluster=cluster)
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_two_c3_replicas_reduced_equal_oracle_sum(tmp_path):
+    # C4's workload per GPU: two C3 replicas (1e6 particles each, key = (1,
+    # replica)) through the HIP engine, one process each on the one GPU,
+    # reduced over gloo; equal to the sum / max of two keyed-oracle windows
+    # (cell-list mode) from the same placements
+    engine = importlib.import_module(PKG + ".engine")
+    workloads = importlib.import_module(PKG + ".workloads")
+    steps = 3
+    out = str(tmp_path / "ens_c3.npz")
+    mp.spawn(_c3_worker, args=(2, _free_port(), out, steps), nprocs=2, join=True)
+    got = np.load(out)
+    ref = []
+    for r in range(2):
+        p = workloads.params("C3", seed=1, replica=r)
+        o = O.Oracle(p, nbmode=O.NB_CELLS)
+        o.set_state(engine.host_init_random(p))
+        ref.append(o.step(steps, want_hashes=False)[0])
+        assert np.array_equal(np.load(out + f".obs{r}.npy"), ref[r]), f"replica {r}"
+    assert not np.array_equal(ref[0], ref[1])
+    sa, ma = ensemble.pack(ref[0])
+    sb, mb = ensemble.pack(ref[1])
+    assert np.array_equal(got["s"], sa + sb)
+    assert np.array_equal(got["m"], np.maximum(ma, mb))

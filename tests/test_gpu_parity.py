@@ -237,3 +237,25 @@ def test_list_overflow_grow_and_replay(monkeypatch, capfd):
     import re
     replays = [int(x) for x in re.findall(r"replays (\d+)", capfd.readouterr().err)]
     assert replays and replays[-1] > 0, "the lists never overflowed: the replay path was not exercised"
+
+
+def test_threshold_rebuild_without_resort(monkeypatch, capfd):
+    # KMC_RESORT=0: no periodic re-sort resets the members[] cursor, so the
+    # rows of the kept complexes (appended on every re-registration) reach
+    # half of members[] and k_finalize latches a full rebuild for the next
+    # step (force_full; k_cx_kill only reads the latch).  The rebuilds must
+    # fire and leave the trajectory unchanged.
+    monkeypatch.setenv("KMC_RESORT", "0")
+    monkeypatch.setenv("KMC_DEBUG_COUNTS", "1")
+    p = params(seed=41, **DENSE)
+    o = O.Oracle(p)
+    o.init_placement()
+    sim = engine.Simulation(p)
+    sim.set_state(o.get_state())
+    obs = np.concatenate([sim.step(1000) for _ in range(4)])
+    obs_o, _ = o.step(4000, want_hashes=False)
+    assert np.array_equal(obs, obs_o)
+    assert engine.state_hash(p, sim.get_state()) == o.hash()
+    import re
+    forced = [int(x) for x in re.findall(r"forced rebuilds (\d+)", capfd.readouterr().err)]
+    assert forced and forced[-1] > 0, "the members[] threshold never fired"

@@ -69,3 +69,36 @@ def test_c3_reaction_heavy_steady_state_window():
     for k in ("complex", "multi", "reject", "rl", "mono", "cis", "rld", "md", "cd", "snap_bond", "snap_cis"):
         assert ev[k] > 0, k
 
+
+
+# C5's regime (VERDICT r02 missing 3): the 1:1 mix and C5's density (10x the
+# reference's area density, L = 5773·sqrt(n_a / 1500)) at 2e5 particles, so
+# that the cell-list oracle can check a bond-rich window in the suite.  C5's
+# reference rates form multi-ligand complexes (main.cpp:974-1732); the dense
+# scenario's rates also fire every dissociation (main.cpp:2063-2141).
+def _c5_regime(seed, **kw):
+    import math
+
+    n = 100000
+    L = 5773.0 * math.sqrt(n / 1500)
+    return engine.capi.default_params(n_a=n, n_b=n, box_x=L, box_y=L, box_z=1000.0, seed=seed, **kw)
+
+
+@pytest.mark.timeout(600)
+def test_c5_regime_steady_state_window():
+    p = _c5_regime(seed=5)
+    ev, obs = _evolved_window(p, 20000, 20)
+    print("  C5-regime window events", ev, file=sys.stderr)
+    assert obs[-1]["bond_num"] > 1000
+    for k in ("complex", "multi", "laydown", "reject", "rl", "snap_bond"):
+        assert ev[k] > 0, k
+
+
+@pytest.mark.timeout(600)
+def test_c5_regime_reaction_heavy_steady_state_window():
+    p = _c5_regime(seed=6, **RATES)
+    ev, obs = _evolved_window(p, 20000, 20)
+    print("  C5-regime-heavy window events", ev, file=sys.stderr)
+    for k in ("complex", "multi", "repeat", "reject", "rl", "mono", "cis", "rld", "md", "cd", "snap_bond",
+              "snap_cis"):
+        assert ev[k] > 0, k
