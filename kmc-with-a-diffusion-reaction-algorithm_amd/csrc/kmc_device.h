@@ -31,6 +31,8 @@ struct KParams {
   int tcap;  // LDS tile record capacity (<= TCAP; lowered only to test the global path)
   int tile;  // cells per tile side of the LDS scans (<= TILE_MAX)
   int dbg_stage;  // debug timing only: stop the tile scans after stage 1 (load) / 2 (items); 0 = off
+  uint32_t cx_limit;  // members[] cursor above which k_finalize latches a full complex rebuild (mcap / 2;
+                      // lowered only by KMC_DEBUG_CX_LIMIT to exercise the rebuild)
 };
 
 // per-step control block in device memory (replayable without host writes)

@@ -308,6 +308,11 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   rc |= dalloc(s, &d.cx_size, NB);
   rc |= dalloc(s, &d.cx_nb, NB);
   d.mcap = (uint32_t)(3 * (size_t)N);
+  K.cx_limit = d.mcap / 2;
+  {
+    const char* cl = getenv("KMC_DEBUG_CX_LIMIT");  // debug: rebuild every complex far earlier
+    if (cl && *cl) K.cx_limit = (uint32_t)std::max(0, std::min((int)K.cx_limit, atoi(cl)));
+  }
   rc |= dalloc(s, &d.members, d.mcap);
   rc |= dalloc(s, &d.shuf, d.mcap);
   rc |= dalloc(s, &d.mrec, d.mcap);

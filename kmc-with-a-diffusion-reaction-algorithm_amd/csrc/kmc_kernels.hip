@@ -881,6 +881,7 @@ struct CxLds {
   int slot[CXL];         // slot of member t
   int res[CXL];          // member row (encoded), shuffled in place like results[c][.]
   uint8_t mv[CXL];       // moved flags of this step (main.cpp:122)
+  uint8_t pos[CXL];      // position of member t in the shuffled row res (wave-parallel alignment)
   uint32_t rnd[CX_SHUF][CXL];  // the first CX_SHUF shuffles' keyed draws, computed by all lanes at once
 };
 struct LdsBeads {
@@ -966,22 +967,17 @@ __device__ __forceinline__ void ligand_template(double rb, double tx[5][3], doub
   tx[4][2] = rb * (s3 / 2 + 1); ty[4][2] = -rb / s3 - rb / 2;
 }
 
-// body of lable4, main.cpp:1441-1583; returns protein_B_index (0-based) after it
+// lable4's re-laying of ligand B flat at receptor a1's height, its site j
+// facing a1 (main.cpp:1441-1520): every new bead is a function of a1's beads
+// and the template only.  bead < 0: all eight beads (one lane); else only
+// bead (m, n) = (bead / 2 + 1, bead % 2 + 1) (lanes of a wave, one bead each)
 template <class CX>
-__device__ __forceinline__ int step2_body(const CX& X, int B, int j, int a1) {
+__device__ __forceinline__ void step2_relayout(const CX& X, int B, int j, int a1, int bead) {
   const KParams& P = X.P;
   const auto& N = X.N;
   const int NA = P.NA;
-  X.set_moved(B);
   int lb = B - NA;
   double za = N.A(a1, 3, 1, 2);
-  for (int k = 1; k <= 2; ++k) {
-    N.B(lb, 1, k, 2) = za;
-    N.B(lb, 2, k, 2) = za;
-    N.B(lb, 3, k, 2) = za;
-    N.B(lb, 4, k, 2) = za;
-  }
-  N.B(lb, 1, 2, 2) = N.A(a1, 3, 1, 2) + P.rb;
   double tx[5][3], ty[5][3];
   ligand_template(P.rb, tx, ty);
   // tx[j][1], ty[j][1] (j = 2..4) without a dynamically indexed array
@@ -998,9 +994,21 @@ __device__ __forceinline__ int step2_body(const CX& X, int B, int j, int a1) {
   double ca = kmcm::cos(angle), sa = kmcm::sin(angle);
   for (int m = 1; m <= 4; ++m)
     for (int n = 1; n <= 2; ++n) {
+      if (bead >= 0 && bead != (m - 1) * 2 + (n - 1)) continue;
+      // z: every bead at za, the normal point [1][2] at za + rb (main.cpp:1441-1452)
+      N.B(lb, m, n, 2) = (m == 1 && n == 2) ? N.A(a1, 3, 1, 2) + P.rb : za;
       N.B(lb, m, n, 0) = tx[m][n] * ca - ty[m][n] * sa + cmx;
       N.B(lb, m, n, 1) = tx[m][n] * sa + ty[m][n] * ca + cmy;
     }
+}
+
+// the rest of lable4 (main.cpp:1521-1583): B's receptors snapped onto its
+// sites, their cis partners onto them; returns protein_B_index (0-based)
+template <class CX>
+__device__ __forceinline__ int step2_sites(const CX& X, int B) {
+  const KParams& P = X.P;
+  const auto& N = X.N;
+  const int NA = P.NA;
   int Bref = B + 1;  // protein_B_index in reference numbering
   for (int m = 2; m <= 4; ++m) {
     int A1ref = X.rnei(Bref, m);
@@ -1022,6 +1030,14 @@ __device__ __forceinline__ int step2_body(const CX& X, int B, int j, int a1) {
     }
   }
   return Bref - 1;
+}
+
+// body of lable4, main.cpp:1441-1583 (one lane); returns protein_B_index (0-based)
+template <class CX>
+__device__ __forceinline__ int step2_body(const CX& X, int B, int j, int a1) {
+  X.set_moved(B);
+  step2_relayout(X, B, j, a1, -1);
+  return step2_sites(X, B);
 }
 
 template <class CX>
@@ -1145,6 +1161,252 @@ __device__ __forceinline__ void multi_ligand_align(const CX& X) {
   }
 }
 
+// wave-level ordering of LDS / global accesses between the lanes of one wave
+// (each wave of the complex kernels works on its own complex: no workgroup
+// barrier)
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// ---------------------------------------------------------------- wave-parallel alignment
+// The lay-down / alignment of a complex staged in LDS (main.cpp:1138-1732)
+// with the lanes of one wave.  Lane t stands for member t (BFS position) in
+// the steps whose iterations touch disjoint beads, so that their order does
+// not matter; the order-dependent parts stay sequential but cheap:
+//  * random_shuffle passes (1285, 1345, 1413, 1597): the row is held one
+//    member per lane and permuted by shuffles across lanes, swap by swap in
+//    the reference's order (the draws are uniform across the wave);
+//  * step 0 / step 3 (1284-1332, 1645-1687): each receptor is tested against
+//    and snapped onto its own ligand site — ligands are not written;
+//  * step 1 (1341-1406): a cis pair of two ligand-bound receptors is handled
+//    by the member met first in the shuffled row among those not yet moved
+//    (pa moves itself onto its partner); pairs are disjoint;
+//  * step 2 + the goto lable4 repeat (1411-1635): the sequential scan over
+//    (member, site) in shuffled order only matters at the positions where
+//    lable4's body runs (it sets the ligand moved, so at most once per
+//    ligand); all (member, site) tests are evaluated at once and a ballot
+//    finds the first position that fires; the body re-lays the ligand one
+//    bead per lane and lane 0 snaps its receptors and their partners;
+//  * step 4 (1691-1732): each ligand-free cis partner is snapped onto its
+//    unique ligand-bound partner.
+// Every value is computed by the same expressions as the one-lane version
+// (complex_align), so the result is bit-identical.  Requires csize <= 64 and
+// 3 * csize <= 64 (CXL).
+
+// one random_shuffle pass over res[0 .. size-2] (libstdc++, main.cpp:1285)
+// on the row held one member per lane
+template <class CX>
+__device__ __forceinline__ int wave_shuffle(const CX& X, int v, uint32_t call, int lane) {
+  uint32_t r = 0;
+  if (lane >= 1 && lane < X.size - 1) r = X.shuf_rand(call, (uint32_t)lane);
+  for (int i = 1; i < X.size - 1; ++i) {
+    const int j = (int)((uint32_t)__shfl((int)r, i, 64) % (uint32_t)(i + 1));
+    if (i != j) {  // uniform
+      const int vi = __shfl(v, i, 64), vj = __shfl(v, j, 64);
+      v = lane == i ? vj : (lane == j ? vi : v);
+    }
+  }
+  return v;
+}
+
+// the shuffled row into LDS (res, and the inverse map pos)
+template <class CX>
+__device__ __forceinline__ void wave_publish_row(const CX& X, CxLds* L, int v, int lane) {
+  if (lane < X.size) {
+    X.res[lane] = v;
+    L->pos[v < X.P.NA ? v : v - X.P.NA] = (uint8_t)lane;
+  }
+  wave_sync();
+}
+
+// steps 0 and 3: receptor m onto its ligand site
+template <class CX>
+__device__ __forceinline__ void wave_snap_bonds(const CX& X, int lane) {
+  const KParams& P = X.P;
+  const int NA = P.NA;
+  const int m = lane;
+  if (m < X.size && m < NA && X.neiA2(m) != 0) {
+    int lb = X.neiA2(m) - 1 - NA, j = X.neiA4(m);
+    if (bond_misaligned(P, X.N, lb, j, m)) {
+      X.set_moved(m);
+      snap_bond(P, X.N, m, lb, j, P.bond_cut);
+    }
+  }
+  wave_sync();
+}
+
+// step 2's test at (member position csi, site j): fires lable4's body
+template <class CX>
+__device__ __forceinline__ bool step2_fires(const CX& X, int B, int j, int& a1) {
+  const KParams& P = X.P;
+  const int NA = P.NA;
+  if (B < NA) return false;
+  int Bref = B + 1;
+  int A1ref = X.rnei(Bref, j);
+  if (!(A1ref != 0 && X.rnei(A1ref, 3) != 0 && X.rnei(X.rnei(A1ref, 3), 2) != 0 && !X.is_moved(B))) return false;
+  a1 = A1ref - 1;
+  double dist2 = dxyBA(X.N, B - NA, j, 2, a1, 3, 2);
+  double dist1 = dxyBA(X.N, B - NA, j, 1, a1, 3, 1);
+  return bond_mis_d(P, dist1, dist2);
+}
+
+// the first (member position, site) at or after candidate c0 (c = csi * 3 +
+// j - 2) whose test fires, or -1; its receptor in a1 (uniform)
+template <class CX>
+__device__ __forceinline__ int step2_first(const CX& X, int v, int c0, int lane, int& a1) {
+  const int c = lane, csi = c / 3, j = 2 + c % 3;
+  const int B = __shfl(v, min(csi, 63), 64);
+  int my_a1 = 0;
+  const bool f = c >= c0 && c < 3 * X.size && step2_fires(X, B, j, my_a1);
+  const uint64_t m = __ballot(f);
+  if (!m) return -1;
+  const int first = __ffsll((unsigned long long)m) - 1;
+  a1 = __shfl(my_a1, first, 64);
+  return first;
+}
+
+// lable4's body at candidate c: the ligand re-laid one bead per lane, then
+// lane 0 snaps its receptors and their partners (main.cpp:1441-1583)
+template <class CX>
+__device__ __forceinline__ void wave_step2_body(const CX& X, int v, int c, int a1, int lane) {
+  const int B = __shfl(v, c / 3, 64), j = 2 + c % 3;
+  if (lane < 8) step2_relayout(X, B, j, a1, lane);
+  if (lane == 0) X.set_moved(B);
+  wave_sync();
+  if (lane == 0) step2_sites(X, B);
+  wave_sync();
+}
+
+template <class CX>
+__device__ __forceinline__ void multi_ligand_align_wave(const CX& X, CxLds* L, int lane) {
+  const KParams& P = X.P;
+  const auto& N = X.N;
+  const int NA = P.NA;
+  const int csize = X.size;
+  uint32_t call = 0;
+  int v = lane < csize ? X.res[lane] : 0;  // the row, one member per lane
+  // step 0
+  v = wave_shuffle(X, v, call++, lane);
+  wave_snap_bonds(X, lane);
+  // step 1: moved flags as left by step 0, read before any is set
+  v = wave_shuffle(X, v, call++, lane);
+  wave_publish_row(X, L, v, lane);
+  {
+    const int pa = lane;
+    bool go = false;
+    int a2 = 0;
+    if (pa < csize && pa < NA && X.neiA2(pa) != 0 && X.neiA3(pa) != 0 && X.rnei(X.neiA3(pa), 2) != 0 &&
+        !X.is_moved(pa)) {
+      a2 = X.neiA3(pa) - 1;
+      go = X.is_moved(a2) || L->pos[pa] < L->pos[a2];  // the partner does not come first
+    }
+    wave_sync();
+    if (go) {
+      X.set_moved(pa);
+      X.set_moved(a2);
+      double dd1 = dxyA(N, pa, 3, 1, a2, 3, 1);
+      double dd2 = dxyA(N, pa, 3, 3, a2, 3, 3);
+      if (!AreSame(dd1, P.cis_cut / 2 + P.ra + P.ra) || !AreSame(dd2, P.cis_cut / 2)) snap_cis(P, N, pa, a2, P.cis_cut);
+    }
+    wave_sync();
+  }
+  // step 2 + repeat
+  v = wave_shuffle(X, v, call++, lane);
+  int c0 = 0;
+  for (int guard = 0;; ++guard) {
+    if (guard > 4 * csize + 8) {
+      if (lane == 0) atomicOr(X.err, ERR_ALIGN);
+      wave_publish_row(X, L, v, lane);
+      return;
+    }
+    for (;;) {  // the pass from c0 to the end
+      int a1 = 0;
+      const int c = step2_first(X, v, c0, lane, a1);
+      if (c < 0) break;
+      wave_step2_body(X, v, c, a1, lane);
+      c0 = c + 1;
+    }
+    v = wave_shuffle(X, v, call++, lane);
+    int a1 = 0;
+    const int c = step2_first(X, v, 0, lane, a1);
+    if (c < 0) break;
+    wave_step2_body(X, v, c, a1, lane);
+    c0 = c + 1;
+  }
+  wave_publish_row(X, L, v, lane);
+  // step 3
+  wave_snap_bonds(X, lane);
+  // step 4
+  {
+    const int m = lane;
+    if (m < csize && m < NA && X.neiA2(m) != 0 && X.neiA3(m) != 0 && X.rnei(X.neiA3(m), 2) == 0) {
+      int a2 = X.neiA3(m) - 1;
+      if (cis_misaligned(P, N, m, a2)) snap_cis(P, N, a2, m, P.cis_cut);
+    }
+    wave_sync();
+  }
+}
+
+// complex_align with the lanes of one wave (staged complex, root = member 0,
+// pA = the last receptor in member order); every lane calls
+template <class CX>
+__device__ __forceinline__ void complex_align_wave(const CX& X, CxLds* L, int nB, int pA, int lane) {
+  const KParams& P = X.P;
+  const auto& N = X.N;
+  if (nB > 1) {
+    multi_ligand_align_wave(X, L, lane);
+    return;
+  }
+  if (nB != 1) return;
+  const int lbB = 0;
+  // lay-down, main.cpp:1140-1193: one bead per lane; the angle and the
+  // centre are read by every lane before any bead is written
+  if (N.B(lbB, 1, 2, 2) != (N.B(lbB, 1, 1, 2) + P.rb)) {
+    double za = N.A(pA, 3, 1, 2);
+    double angle = kmcm::atan2((N.B(lbB, 2, 1, 0) - N.B(lbB, 1, 1, 0)), (N.B(lbB, 2, 1, 1) - N.B(lbB, 1, 1, 1))) + P.pai;
+    double tx[5][3], ty[5][3];
+    ligand_template(P.rb, tx, ty);
+    double l0x = N.B(lbB, 1, 1, 0), l0y = N.B(lbB, 1, 1, 1);
+    double ca = kmcm::cos(angle), sa = kmcm::sin(angle);
+    wave_sync();
+    for (int j = 1; j <= 4; ++j)
+      for (int k = 1; k <= 2; ++k) {
+        if (lane != (j - 1) * 2 + (k - 1)) continue;
+        N.B(lbB, j, k, 2) = (j == 1 && k == 2) ? N.A(pA, 3, 1, 2) + P.rb : za;
+        N.B(lbB, j, k, 0) = tx[j][k] * ca - ty[j][k] * sa + l0x;
+        N.B(lbB, j, k, 1) = tx[j][k] * sa + ty[j][k] * ca + l0y;
+      }
+    wave_sync();
+  }
+  // attached receptors (main.cpp:1196-1233): lane j - 2, distinct receptors
+  const int j = lane + 2;
+  int a1ref = 0;
+  if (lane < 3) {
+    a1ref = X.neiB(lbB, j);
+    if (a1ref != 0 && bond_misaligned(P, N, lbB, j, a1ref - 1)) snap_bond(P, N, a1ref - 1, lbB, j, P.bond_cut);
+  }
+  wave_sync();
+  // their cis partners (1237-1274): in parallel unless a partner is itself
+  // one of the ligand's receptors (then the site order decides: one lane)
+  int a2ref = 0;
+  if (lane < 3 && a1ref != 0) a2ref = X.neiA3(a1ref - 1);
+  const int r2 = __shfl(a1ref, 0, 64), r3 = __shfl(a1ref, 1, 64), r4 = __shfl(a1ref, 2, 64);
+  const bool clash = a2ref != 0 && (a2ref == r2 || a2ref == r3 || a2ref == r4);
+  if (__ballot(clash) == 0) {
+    if (a2ref != 0 && cis_misaligned(P, N, a1ref - 1, a2ref - 1)) snap_cis(P, N, a2ref - 1, a1ref - 1, P.cis_cut);
+  } else if (lane == 0) {
+    for (int jj = 2; jj <= 4; ++jj) {
+      int b1 = X.neiB(lbB, jj);
+      if (b1 != 0 && X.neiA3(b1 - 1) != 0) {
+        int a1 = b1 - 1, a2 = X.neiA3(a1) - 1;
+        if (cis_misaligned(P, N, a1, a2)) snap_cis(P, N, a2, a1, P.cis_cut);
+      }
+    }
+  }
+  wave_sync();
+}
+
 // lay-down + alignment on lane 0, main.cpp:1138-1732 (lbB: store index of the
 // root ligand, pA: of the last receptor in member order)
 template <class CX>
@@ -1187,13 +1449,6 @@ __device__ __forceinline__ void complex_align(const CX& X, int nB, int lbB, int 
   }
 }
 
-// wave-level ordering of LDS / global accesses between the lanes of one wave
-// (each wave of the complex kernels works on its own complex: no workgroup
-// barrier)
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-}
 
 // LDS image of a complex (lanes < csize) from the member records
 // register_complex stored: slots and links encoded by BFS position (one
@@ -1638,15 +1893,14 @@ __global__ void __launch_bounds__(256) k_complex_heavy(KParams P, Dev d) {
           L->rnd[call][pos] = kmcr::rand31(P.key, kmcr::DOM_SHUF, (uint32_t)desc.w, call, step, pos);
       }
     wave_sync();
-    if (lane == 0) {
-      int pA = -1;  // last receptor in member order
-      for (int q = csize - 1; q >= 0 && pA < 0; --q)
-        if (L->slot[q] < NA) pA = q;
+    {
+      // the last receptor in member order: the highest lane holding one
+      const uint64_t rm = __ballot(lane < csize && L->slot[lane] < NA);
+      const int pA = rm ? 63 - __clzll((long long)rm) : -1;
       CxT<LdsBeads, LdsLinks> X{P, step, (uint32_t)desc.w, L->res, csize, LdsBeads{L}, LdsLinks{L, NA}, &d.ctl->err,
                                 L->rnd};
-      complex_align(X, nB, 0, pA);  // the root is member 0
+      complex_align_wave(X, L, nB, pA, lane);  // the root is member 0
     }
-    wave_sync();
     cx_write_back(d, L, d.shuf + desc.y, csize, nB, NA, lane);  // shuffled row: shuf (members keeps BFS order)
     if (nB > 1 && lane == 0) d.shuf_tag[lb] = step;
     cx_count(P, d, L, csize, lane, lane < csize ? d.rank[L->slot[lane]].x : 0);  // old rank: k_move_members
@@ -3006,7 +3260,7 @@ __global__ void __launch_bounds__(256) k_finalize(KParams P, Dev d, double time_
   }
   // the next step's k_cx_kill: rebuild every complex when the appended rows
   // fill half of members[] or this step's dirty list overflowed
-  const uint32_t ff = (c->cx_cursor > d.mcap / 2 || c->n_dirty[step & 1] > (uint32_t)P.N) ? 1u : 0u;
+  const uint32_t ff = (c->cx_cursor > P.cx_limit || c->n_dirty[step & 1] > (uint32_t)P.N) ? 1u : 0u;
   c->force_full = ff;
   c->n_forced += ff;
   c->maxc = maxc;

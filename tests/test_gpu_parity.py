@@ -242,10 +242,12 @@ def test_list_overflow_grow_and_replay(monkeypatch, capfd):
 def test_threshold_rebuild_without_resort(monkeypatch, capfd):
     # KMC_RESORT=0: no periodic re-sort resets the members[] cursor, so the
     # rows of the kept complexes (appended on every re-registration) reach
-    # half of members[] and k_finalize latches a full rebuild for the next
-    # step (force_full; k_cx_kill only reads the latch).  The rebuilds must
-    # fire and leave the trajectory unchanged.
+    # the limit (half of members[]; lowered here to 64 entries so that it
+    # fires within the window) and k_finalize latches a full rebuild for the
+    # next step (force_full; k_cx_kill only reads the latch).  The rebuilds
+    # must fire and leave the trajectory unchanged.
     monkeypatch.setenv("KMC_RESORT", "0")
+    monkeypatch.setenv("KMC_DEBUG_CX_LIMIT", "64")
     monkeypatch.setenv("KMC_DEBUG_COUNTS", "1")
     p = params(seed=41, **DENSE)
     o = O.Oracle(p)
