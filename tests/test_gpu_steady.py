@@ -39,7 +39,10 @@ def _evolved_window(p, evolve, window):
     sim.close()
     o = O.Oracle(p, nbmode=O.NB_CELLS)
     o.set_state(st)
-    obs_o, _ = o.step(window, want_hashes=False)
+    obs_o = []
+    for s in range(window):  # one step at a time: a progress line per oracle step
+        obs_o.append(o.step(1, want_hashes=False)[0][0])
+        print(f"  oracle step {evolve + s + 1} ({time.time() - t:.0f}s)", file=sys.stderr, flush=True)
     for s in range(window):
         assert obs[s] == obs_o[s], f"step {evolve + s + 1}: gpu {obs[s]} oracle {obs_o[s]}"
     assert h == o.hash()

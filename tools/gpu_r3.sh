@@ -15,7 +15,7 @@ cd "$root"
 if [ "$kexpr" != "SKIP" ]; then
   K=()
   [ "$kexpr" != "ALL" ] && K=(-k "$kexpr")
-  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread "${K[@]}" \
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v -s --timeout 600 --timeout-method thread "${K[@]}" \
     > "$out/tests.log" 2>&1
 fi
 timeout -k 10 500 python bench.py > "$out/bench.json" 2> "$out/bench.err"
