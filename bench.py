@@ -57,13 +57,10 @@ def kernel_bytes(name: str, n_a: int, n_b: int):
     models = {
         # the proposal phase (PROPOSE_PHASE): every protein's R read (16
         # receptor / 8 ligand beads × xyz × 8 B) and R_new written, its unit
-        # kind read, its record ranks written
-        "k_propose": 768 * n_a + 384 * n_b + n + 8 * n,
+        # kind and home position read, its two 32-byte records written
+        "k_propose": 768 * n_a + 384 * n_b + n + 8 * n + 64 * n,
         # every record once (float4 + id + site)
         "k_pair_scan": 2 * n * 32,
-        # old + new reference points (x, y, zlo, zhi) + receptor site, record
-        # write (pos, id, site), owner, cell cursor
-        "k_rec_scatter": 2 * n * 32 + 2 * n_a * 16 + 2 * n * 32 + 4 * n + 2 * n * 8,
         "k_commit": 8 * n,
         "k_classify": 20 * n_a + 12 * n_b + 5 * n,
         "k_observe": 16 * n_a + 5 * n_b,

@@ -31,6 +31,7 @@ struct KParams {
   int tcap;  // LDS tile record capacity (<= TCAP; lowered only to test the global path)
   int tile;  // cells per tile side of the LDS scans (<= TILE_MAX)
   int dbg_stage;  // debug timing only: stop the tile scans after stage 1 (load) / 2 (items); 0 = off
+  int cx_serial;  // debug: complexes aligned by one lane (KMC_CX_SERIAL=1) instead of the whole wave
   uint32_t cx_limit;  // members[] cursor above which k_finalize latches a full complex rebuild (mcap / 2;
                       // lowered only by KMC_DEBUG_CX_LIMIT to exercise the rebuild)
 };
@@ -54,6 +55,7 @@ struct Ctl {
   uint32_t last[8];       // previous step's work counts (diagnostics): cand conf plist rej pairs rl cisc overflow
   uint32_t n_rl;          // R–L accepting edges
   uint32_t n_cisc;        // cis candidates
+  uint32_t n_outl;        // records listed on the outlier list this step (more than a cell from home)
   // observable bookkeeping (the per-step counts are reduced by k_finalize)
   int32_t off_bond, off_rl, off_cis, off_mono;  // counters − derived at load
   int32_t maxc;                                 // protein_num_in_Max_Complex

@@ -19,15 +19,14 @@ using namespace kmcd;
 
 // kernel ids for per-kernel HIP-event timing (kmc_set_timing / kmc_kernel_times)
 enum KId {
-  KI_CLASSIFY, KI_BFS, KI_PROPOSE, KI_PROPOSE_FREE, KI_MOVE_MEMBERS, KI_CX_CHECK, KI_CX_HEAVY, KI_CX_KILL, KI_SCAN,
-  KI_REC_SCATTER,
+  KI_CLASSIFY, KI_BFS, KI_PROPOSE, KI_PROPOSE_FREE, KI_MOVE_MEMBERS, KI_CX_CHECK, KI_CX_HEAVY, KI_CX_KILL,
   KI_PAIR_SCAN, KI_COL_EXACT, KI_COL_ROUNDS, KI_COMMIT, KI_RXN_EXACT, KI_MATCH, KI_DISS_OBSERVE,
   KI_RESORT, KI_N
 };
 static const char* const KNAMES[KI_N] = {
     "k_classify", "k_bfs", "k_propose", "k_propose_free", "k_move_members", "k_cx_check", "k_complex_heavy",
-    "k_cx_kill", "k_scan",
-    "k_rec_scatter", "k_pair_scan", "k_col_exact", "k_col_rounds", "k_commit", "k_rxn_exact",
+    "k_cx_kill",
+    "k_pair_scan", "k_col_exact", "k_col_rounds", "k_commit", "k_rxn_exact",
     "k_match", "k_diss_observe", "slot_resort"};
 #define TRING 64  // steps of event pairs kept in flight
 
@@ -71,8 +70,9 @@ struct kmc_sim {
   int32_t *a_tmp = nullptr, *b_tmp = nullptr, *id_tmp = nullptr;
   void* sort_tmp = nullptr;
   size_t sort_tmp_bytes = 0;
-  void* scan_tmp = nullptr;  // hipcub exclusive scan of the cell counts
+  void* scan_tmp = nullptr;  // hipcub exclusive scan of the home cell counts (home_build)
   size_t scan_tmp_bytes = 0;
+  int32_t* hcnt = nullptr;   // [ncell+1] home cell counts (home_build)
   // per-kernel timing: a ring of TRING steps of event pairs, read back lazily
   uint64_t tmask = 0;
   int32_t tperiod = 1;    // bracket only every tperiod-th step
@@ -162,6 +162,7 @@ int alloc_lists(kmc_sim* s) {
   dfree(s, d.ent);
   dfree(s, d.gi32);
   dfree(s, d.pq_ent);
+  dfree(s, d.outl);
   uint32_t cap = (uint32_t)scale(pow2(std::max<uint32_t>(4096, std::min<uint32_t>(1u << 20, (uint32_t)N / 8 + 1))));
   d.cap_edges = pow2(cap);
   int rc = KMC_OK;
@@ -182,6 +183,10 @@ int alloc_lists(kmc_sim* s) {
   rc |= dalloc(s, &d.ent, (size_t)2 * d.cap_edges);
   rc |= dalloc(s, &d.gi32, (size_t)6 * d.cap_edges);
   rc |= dalloc(s, &d.pq_ent, (size_t)d.conf.cap * NSHARD);
+  // records more than a cell from their home cell: none at the benchmark
+  // densities between re-sorts (a protein drifts a few Å per step)
+  d.outl_cap = (uint32_t)scale(std::max<uint64_t>(1024, N / 64));
+  rc |= dalloc(s, &d.outl, d.outl_cap);
   return rc;
 }
 
@@ -326,10 +331,9 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   rc |= dalloc(s, &d.overflow, NB);
   rc |= dalloc(s, &d.cx_list, (size_t)d.mcap / 2);  // kept across steps: every registration since the last rebuild
   rc |= dalloc(s, &d.cx_heavy, NB);
-  rc |= dalloc(s, &d.cell_cnt, s->ncell + 1);
-  rc |= dalloc(s, &d.cell_cnt_alt, s->ncell + 1);
-  d.ncnt = s->ncell + 1;
-  rc |= dalloc(s, &d.cell_start, s->ncell + 1);
+  rc |= dalloc(s, &s->hcnt, s->ncell + 1);
+  rc |= dalloc(s, &d.hstart, s->ncell + 1);
+  rc |= dalloc(s, &d.home, N);
   rc |= dalloc(s, &d.rec, (size_t)2 * N);
   rc |= dalloc(s, &d.shard_cnt, (size_t)5 * NSHARD);
   {
@@ -337,7 +341,6 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
     s->grow = cs && *cs ? -std::max(0, std::min(20, atoi(cs))) : 0;
   }
   rc |= alloc_lists(s);
-  rc |= dalloc(s, &d.rank, N);
   rc |= dalloc(s, &d.pq_units, N);
   rc |= dalloc(s, &d.obs_part, (size_t)8 * ((N + 255) / 256));
   rc |= dalloc(s, &d.bfs_queue, N);
@@ -372,12 +375,13 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
     s->always_full = fb && *fb == '1';
     const char* ds = getenv("KMC_DEBUG_SCAN_STAGE");
     K.dbg_stage = ds && *ds ? atoi(ds) : 0;
+    const char* cxs = getenv("KMC_CX_SERIAL");
+    K.cx_serial = cxs && *cxs == '1';
     const char* gr = getenv("KMC_GRAPH");
     s->use_graphs = gr && *gr == '1';
   }
   {
-    const uint64_t ntx = (K.ncx + K.tile - 1) / K.tile, nty = (K.ncy + K.tile - 1) / K.tile;
-    const uint64_t kmax = ntx * nty * (uint64_t)K.tile * K.tile;
+    const uint64_t kmax = (uint64_t)K.ncx * K.ncy;  // row-major cell keys (k_slot_keys)
     s->key_bits = 1;
     while ((1ull << s->key_bits) < kmax) ++s->key_bits;
     const char* re = getenv("KMC_RESORT");
@@ -397,7 +401,7 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
       return KMC_ERR_HIP;
     }
     tb = 0;
-    if (hipcub::DeviceScan::ExclusiveSum(nullptr, tb, s->d.cell_cnt, s->d.cell_start, s->ncell + 1, s->stream) !=
+    if (hipcub::DeviceScan::ExclusiveSum(nullptr, tb, s->hcnt, s->d.hstart, s->ncell + 1, s->stream) !=
         hipSuccess) {
       kmc_destroy(s);
       return KMC_ERR_HIP;
@@ -460,7 +464,23 @@ __global__ void k_iota(int32_t* a, int32_t* b, int n) {
   if (i < n) a[i] = b[i] = i;
 }
 
-// Re-sort the slots spatially (between steps; R_new is free scratch then).
+// Home list (kmc_kernels.hip §records): every slot's home cell and position
+// from R, counting sort by cell; hstart = the cells' first home positions.
+static int home_build(kmc_sim* s) {
+  const KParams& K = s->K;
+  Dev& d = s->d;
+  hipStream_t st = s->stream;
+  const int N = K.N, T = 256;
+  HIPCHK(s, hipMemsetAsync(s->hcnt, 0, sizeof(int32_t) * (size_t)(s->ncell + 1), st));
+  k_home_count<<<(N + T - 1) / T, T, 0, st>>>(K, d, s->hcnt);
+  size_t tb = s->scan_tmp_bytes;
+  HIPCHK(s, hipcub::DeviceScan::ExclusiveSum(s->scan_tmp, tb, s->hcnt, d.hstart, s->ncell + 1, st));
+  k_home_place<<<(N + T - 1) / T, T, 0, st>>>(K, d);
+  return hipGetLastError() == hipSuccess ? KMC_OK : fail(s, KMC_ERR_HIP, "home_build launch");
+}
+
+// Re-sort the slots spatially (between steps; R_new is free scratch then),
+// then rebuild the home list in the new slot numbering.
 static int resort(kmc_sim* s) {
   const KParams& K = s->K;
   Dev& d = s->d;
@@ -480,7 +500,8 @@ static int resort(kmc_sim* s) {
   reorder(s, s->perm, s->newslot, true);
   k_gather_ids<<<(N + T - 1) / T, T, 0, st>>>(K, d.id_of, s->id_tmp, d.slot_of, s->perm);
   std::swap(d.id_of, s->id_tmp);
-  return hipGetLastError() == hipSuccess ? KMC_OK : fail(s, KMC_ERR_HIP, "resort launch");
+  if (hipGetLastError() != hipSuccess) return fail(s, KMC_ERR_HIP, "resort launch");
+  return home_build(s);
 }
 
 // Every array that carries a step / round tag or a per-step count: a state
@@ -493,8 +514,6 @@ static int clear_step_tags(kmc_sim* s) {
   HIPCHK(s, hipMemsetAsync(d.moved, 0, sizeof(uint32_t) * N, st));
   HIPCHK(s, hipMemsetAsync(d.pend, 0, sizeof(uint32_t) * N, st));
   HIPCHK(s, hipMemsetAsync(d.vtag, 0, sizeof(uint32_t) * N, st));
-  HIPCHK(s, hipMemsetAsync(d.cell_cnt, 0, sizeof(int32_t) * (size_t)d.ncnt, st));
-  HIPCHK(s, hipMemsetAsync(d.cell_cnt_alt, 0, sizeof(int32_t) * (size_t)d.ncnt, st));
   HIPCHK(s, hipMemsetAsync(d.shard_cnt, 0, sizeof(uint32_t) * 5 * NSHARD, st));
   // BFS candidates and shuffled rows are tagged with the step: an undone
   // chunk's tags would match the replayed steps' numbers
@@ -532,7 +551,11 @@ static int snapshot(kmc_sim* s, bool restore) {
   HIPCHK(s, cp(d.id_of, s->snap_id, sizeof(int32_t) * N));
   HIPCHK(s, cp(d.slot_of, s->snap_slot, sizeof(int32_t) * N));
   HIPCHK(s, cp(d.ctl, s->snap_ctl, sizeof(Ctl)));
-  return restore ? clear_step_tags(s) : KMC_OK;
+  if (!restore) return KMC_OK;
+  // the undone chunk may have re-sorted: the home list must describe the
+  // restored slot numbering
+  const int rc = clear_step_tags(s);
+  return rc != KMC_OK ? rc : home_build(s);
 }
 
 int kmc_set_state(kmc_sim* s, const kmc_state_view* v) {
@@ -757,14 +780,6 @@ static int launch_step(kmc_sim* s, bool re_sort) {
       TIMED(KI_CX_HEAVY, (k_complex_heavy<<<1024, T, 0, st>>>(K, d)));
     }
   }
-  TIMED(KI_SCAN, {
-    // single-pass decoupled look-back scan; cell_cnt[ncell] stays 0, so
-    // cell_start[ncell] is the record total (a hand-written single-launch
-    // look-back scan measured 24 µs against hipcub's 5 + 13 µs at C3)
-    size_t tb = s->scan_tmp_bytes;
-    (void)hipcub::DeviceScan::ExclusiveSum(s->scan_tmp, tb, d.cell_cnt, d.cell_start, s->ncell + 1, st);
-  });
-  TIMED(KI_REC_SCATTER, (k_rec_scatter<<<gN, T, 0, st>>>(K, d)));
   const int gX = std::min(2048, (K.N + T - 1) / T);  // grid-stride kernels over device-sized lists
   const int ntiles = ((K.ncx + K.tile - 1) / K.tile) * ((K.ncy + K.tile - 1) / K.tile);
   // collision candidates and reaction candidates, one staging of each tile
@@ -787,7 +802,6 @@ static int launch_step(kmc_sim* s, bool re_sort) {
   if (s->tnow) s->tslot = (s->tslot + 1) % TRING;
   // R_new becomes R (main.cpp:2164-2191): swap the bead buffers
   std::swap(d.cur, d.nxt);
-  std::swap(d.cell_cnt, d.cell_cnt_alt);
   return KMC_OK;
 }
 
@@ -802,7 +816,6 @@ static int launch_step_graph(kmc_sim* s) {
     if (g.valid && std::memcmp(g.key, key, sizeof key) == 0) {
       HIPCHK(s, hipGraphLaunch(g.exec, s->stream));
       std::swap(s->d.cur, s->d.nxt);
-      std::swap(s->d.cell_cnt, s->d.cell_cnt_alt);
       ++s->graph_launches;
       return KMC_OK;
     }

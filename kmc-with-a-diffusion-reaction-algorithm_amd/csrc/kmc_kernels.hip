@@ -70,11 +70,15 @@ struct Dev {
   int4* cx_list;     // [NB] descriptors of the registered complexes (kept across steps; cx_params, k_cx_check)
   int4* cx_heavy;    // [NB] descriptors for k_complex_heavy: larger complexes, and those k_cx_check
                      //      moved but whose lay-down / alignment changes beads
-  int32_t* cell_cnt;    // [ncell+1] this step's record counts (counted by the proposals, read by the scan)
-  int32_t* cell_cnt_alt;  // [ncell+1] the next step's counts: zeroed by k_diss_observe, swapped after the step
-  int ncnt;             // ncell+1
-  int32_t* cell_start;  // [ncell+1]
-  struct Rec* rec;      // [2N] cell-sorted records (old and proposed position of every protein)
+  // Home list (§records): every protein has a home position hp in an order
+  // sorted by its home cell — the cell of its reference point at the last
+  // re-sort — and its two records of a step (old and proposed position) live
+  // at rec[2 hp], rec[2 hp + 1].  Rebuilt only with the slot order.
+  uint2* home;          // [N] slot -> {hp, home cell cx | cy << 16}
+  int32_t* hstart;      // [ncell+1] first home position of each (row, kind, column) cell
+  struct Rec* rec;      // [2N] records, home order; written by the kernels that move the protein
+  int4* outl;           // [outl_cap] records more than one cell from their home cell: {record, cx, cy, -}
+  uint32_t outl_cap;
   SList cand;           // collision candidates (proposal record, other record)
   SList conf;           // conflict entries (u, kq | isnew<<31)
   SList plist;          // units with conflict entries (u, 0)
@@ -83,7 +87,6 @@ struct Dev {
   int32_t* pq_units;    // [N] units still pending after the grid round (k_col_units)
   int2* pq_ent;         // [conf capacity] conflict entries left pending by round 0 (k_col_round)
   uint32_t* shard_cnt;  // [5][NSHARD] counters of the lists above
-  int2* rank;           // [N] rank of the old / proposed record within its cell
   int32_t* obs_part;    // [blocks][8] per-block observable partials
   uint64_t* rl_keys;    // [cap]
   uint64_t* cis_keys;   // [cap]
@@ -96,12 +99,19 @@ struct Dev {
   struct kmc_obs_dev* obs;
 };
 
-// one cell-sorted record (32 B): float reference point, ids, cis site
+// one record (32 B): float reference point, ids, cis site
 struct alignas(16) Rec {
   float4 pos;   // x, y of bead [1][1]; z span (receptor: lowest/highest domain; ligand: centre)
-  int2 id;      // {pid | st3<<29 | st2<<30 | isnew<<31, owner key}
+  int2 id;      // {slot | cell code << 25 | st3 << 29 | st2 << 30 | isnew << 31, owner key}
   float2 site;  // receptor [3][3] site xy (reaction prefilter); 0 for ligands
 };
+#define RID_PID 0x00ffffff
+#define RID_CODE_SHIFT 25  // 4-bit cell code: (dy + 1) * 3 + (dx + 1), the record's cell relative to its home
+                           // cell; RID_OUT: more than one cell away (the record is on the outlier list)
+#define RID_OUT 15
+#define RID_ST3 (1 << 29)
+#define RID_ST2 (1 << 30)
+__device__ __forceinline__ int rec_code(int2 id) { return (id.x >> RID_CODE_SHIFT) & 15; }
 
 struct kmc_obs_dev {  // == kmc_obs
   int64_t step;
@@ -528,39 +538,74 @@ __device__ __forceinline__ bool extent_ok(const Beads& B, int p, int NA) {
   return true;
 }
 
-// sort key of a record: (cell row, kind, cell column), see §LDS tiles
-__device__ __forceinline__ int rec_cell(const KParams& P, double x, double y, int kind) {
-  return (cell_y(P, y) * 2 + kind) * P.ncx + cell_x(P, x);
+// cell index of the (row, kind, column) cell order of the home list
+__device__ __forceinline__ int cell_index(const KParams& P, int cx, int cy, int kind) {
+  return (cy * 2 + kind) * P.ncx + cx;
 }
 
+// ---------------------------------------------------------------- records
+// The neighbour searches (collisions main.cpp:640-664, 1762-1828; reactions
+// 1877-2058) work on records: one per protein and position (old, proposed),
+// written by the kernel that moves the protein, straight from the registers
+// that hold its beads — no per-step counting sort.  Record w of slot p lives
+// at rec[2·hp + w], hp = the protein's home position: the home list orders
+// the proteins by the cell of their reference point at the last re-sort (the
+// home cell; k_home_*).  A protein moves a few Å per step, so between
+// re-sorts a record stays within one cell of its home cell: the record keeps
+// that offset (4-bit cell code), and a tile of the pair scan finds every
+// record of its cells (+ one-cell halo) among the home cells of the tile +
+// two cells.  A record further away (rare: re-sorts every 100 steps) goes
+// onto the outlier list that every tile also reads.
+__device__ __forceinline__ void put_rec(const KParams& P, const Dev& d, uint2 h, int p, int w, int st, int own,
+                                        double x, double y, double zlo, double zhi, double sx, double sy) {
+  const int cx = cell_x(P, x), cy = cell_y(P, y);
+  const int dx = cx - (int)(h.y & 0xffffu), dy = cy - (int)(h.y >> 16);
+  const int ri = 2 * (int)h.x + w;
+  int code = RID_OUT;
+  if (dx >= -1 && dx <= 1 && dy >= -1 && dy <= 1) {
+    code = (dy + 1) * 3 + (dx + 1);
+  } else {
+    const uint32_t o = atomicAdd(&d.ctl->n_outl, 1u);
+    if (o < d.outl_cap) d.outl[o] = make_int4(ri, cx, cy, 0);
+    else atomicOr(&d.ctl->err, ERR_EDGES);
+  }
+  Rec r;
+  r.pos = make_float4((float)x, (float)y, (float)zlo, (float)zhi);
+  r.id = make_int2(p | code << RID_CODE_SHIFT | st | (w << 31), own);
+  r.site = make_float2((float)sx, (float)sy);
+  d.rec[ri] = r;
+}
 
-// A protein's two records (old and proposed position) are counted into their
-// cells by the thread that wrote the proposal (k_propose_free / k_cx_check /
-// k_complex_heavy); the
-// rank within the cell is kept for the scatter.
-__device__ __forceinline__ void count_records(const KParams& P, const Dev& d, int p) {
-  double x, y, zl, zh;
-  int2 rk;
-  const int kind = p >= P.NA;
-  ref_point(d, d.cur, p, P.NA, x, y, zl, zh);
-  rk.x = atomicAdd(&d.cell_cnt[rec_cell(P, x, y, kind)], 1);
-  ref_point(d, d.nxt, p, P.NA, x, y, zl, zh);
-  rk.y = atomicAdd(&d.cell_cnt[rec_cell(P, x, y, kind)], 1);
-  d.rank[p] = rk;
+// status bits of slot p's records
+__device__ __forceinline__ int rec_status(const KParams& P, const Dev& d, int p) {
+  const int NA = P.NA;
+  return p < NA ? (A_ST2(d, p) ? RID_ST2 : 0) | (A_ST3(d, p) ? RID_ST3 : 0) : 0;
+}
+
+// record w of slot p from its beads in global memory (old: R, proposal: R_new)
+__device__ __forceinline__ void put_rec_glb(const KParams& P, const Dev& d, uint2 h, int p, int w, int st, int own) {
+  const Beads& B = w ? d.nxt : d.cur;
+  double x, y, zl, zh, sx = 0.0, sy = 0.0;
+  ref_point(d, B, p, P.NA, x, y, zl, zh);
+  if (p < P.NA) {
+    const double2 s33 = B.Axy(p, 3, 3);
+    sx = s33.x;
+    sy = s33.y;
+  }
+  put_rec(P, d, h, p, w, st, own, x, y, zl, zh, sx, sy);
+}
+
+// both records of slot p from global memory, and the extent bound of its
+// proposal (DESIGN.md §cell list)
+__device__ __forceinline__ void put_recs_glb(const KParams& P, const Dev& d, int p) {
+  const uint2 h = d.home[p];
+  const int st = rec_status(P, d, p), own = d.owner[p];
+  put_rec_glb(P, d, h, p, 0, st, own);
+  put_rec_glb(P, d, h, p, 1, st, own);
   if (!extent_ok(d.nxt, p, P.NA)) atomicOr(&d.ctl->err, ERR_GEOMETRY);
 }
 
 // ================================================================ 2. proposals
-// one protein's records counted from reference points held in registers:
-// the old record's rank was taken before the move (its atomic's latency
-// overlaps the proposal), the new record's here; ext: extent bound of the
-// proposal (DESIGN.md §cell list)
-__device__ __forceinline__ void count_new(const KParams& P, const Dev& d, int p, int rk_old, double nx, double ny,
-                                          bool ext) {
-  const int rk_new = atomicAdd(&d.cell_cnt[rec_cell(P, nx, ny, p >= P.NA)], 1);
-  d.rank[p] = make_int2(rk_old, rk_new);
-  if (!ext) atomicOr(&d.ctl->err, ERR_GEOMETRY);
-}
 
 // free receptor, main.cpp:584-635.  All 48 coordinates are loaded (24 16-byte
 // rows) before the first store (R and R_new are distinct buffers), so a lane
@@ -583,7 +628,7 @@ __device__ void propose_free_a(const KParams& P, const Dev& d, int i, uint32_t s
       r[2 * h][k][2] = v.x;
       r[2 * h + 1][k][2] = v.y;
     }
-  const int rk_old = atomicAdd(&d.cell_cnt[rec_cell(P, r[0][0][0], r[0][0][1], 0)], 1);
+  const uint2 h = d.home[i];
   double u0, u1, u2, u3;
   const uint32_t ri = (uint32_t)d.id_of[i];
   kmcr::uniform2(P.key, kmcr::DOM_DIFF, ri, 0, step, 0, &u0, &u1);
@@ -595,7 +640,7 @@ __device__ void propose_free_a(const KParams& P, const Dev& d, int i, uint32_t s
   double PBx = P.box_x * kmcm::round_(o11x / P.box_x);
   double PBy = P.box_y * kmcm::round_(o11y / P.box_y);
   Rot t = euler(0, 0, (2 * u2 - 1) * P.rot_a);
-  double ncx[4], ncy[4], nz[4][4];
+  double ncx[4], ncy[4], nz[4][4], nsx = 0.0, nsy = 0.0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     double cx = (r[j][0][0] + dx) - PBx;
@@ -610,7 +655,12 @@ __device__ void propose_free_a(const KParams& P, const Dev& d, int i, uint32_t s
       double ox = (r[j][k][0] + dx) - PBx;
       double oy = (r[j][k][1] + dy) - PBy;
       double oz = r[j][k][2];
-      st_n(d.nxt.A2(i, j * 4 + k), make_double2(rx(t, ox, oy, oz, cx, cy, cz), ry(t, ox, oy, oz, cx, cy, cz)));
+      const double nx = rx(t, ox, oy, oz, cx, cy, cz), ny = ry(t, ox, oy, oz, cx, cy, cz);
+      st_n(d.nxt.A2(i, j * 4 + k), make_double2(nx, ny));
+      if (j == 2 && k == 2) {  // the [3][3] cis site (reaction prefilter)
+        nsx = nx;
+        nsy = ny;
+      }
       nz[j][k] = rz(t, ox, oy, oz, cx, cy, cz);
     }
   }
@@ -624,7 +674,13 @@ __device__ void propose_free_a(const KParams& P, const Dev& d, int i, uint32_t s
     double ex = ncx[j] - ncx[0], ey = ncy[j] - ncy[0];
     ext &= ex * ex + ey * ey <= 0.09;
   }
-  count_new(P, d, i, rk_old, ncx[0], ncy[0], ext);
+  if (!ext) atomicOr(&d.ctl->err, ERR_GEOMETRY);
+  // records: z span of the four domain centres (ref_point), [3][3] site
+  const int own = (int)ri;  // a free receptor is its own unit, status bits 0
+  put_rec(P, d, h, i, 0, 0, own, r[0][0][0], r[0][0][1], fmin(fmin(r[0][0][2], r[1][0][2]), fmin(r[2][0][2], r[3][0][2])),
+          fmax(fmax(r[0][0][2], r[1][0][2]), fmax(r[2][0][2], r[3][0][2])), r[2][2][0], r[2][2][1]);
+  put_rec(P, d, h, i, 1, 0, own, ncx[0], ncy[0], fmin(fmin(nz[0][0], nz[1][0]), fmin(nz[2][0], nz[3][0])),
+          fmax(fmax(nz[0][0], nz[1][0]), fmax(nz[2][0], nz[3][0])), nsx, nsy);
 }
 
 // snap receptor a2 onto a1's cis site (x,y of all 16 beads), main.cpp:786-798
@@ -765,7 +821,7 @@ __device__ void propose_free_b(const KParams& P, const Dev& d, int lb, int p, ui
       r[2 * h][k][2] = v.x;
       r[2 * h + 1][k][2] = v.y;
     }
-  const int rk_old = atomicAdd(&d.cell_cnt[rec_cell(P, r[0][0][0], r[0][0][1], 1)], 1);
+  const uint2 h = d.home[p];
   double u[6];
   const uint32_t rp = (uint32_t)d.id_of[p];
   kmcr::uniform2(P.key, kmcr::DOM_DIFF, rp, 0, step, 0, &u[0], &u[1]);
@@ -827,7 +883,10 @@ __device__ void propose_free_b(const KParams& P, const Dev& d, int lb, int p, ui
     double ex = scx[j] - scx[0], ey = scy[j] - scy[0];
     ext &= ex * ex + ey * ey <= 35.0 * 35.0;
   }
-  count_new(P, d, p, rk_old, scx[0], scy[0], ext);
+  if (!ext) atomicOr(&d.ctl->err, ERR_GEOMETRY);
+  // records: the centre [1][1] (a free ligand is its own unit)
+  put_rec(P, d, h, p, 0, 0, (int)rp, r[0][0][0], r[0][0][1], r[0][0][2], r[0][0][2], 0.0, 0.0);
+  put_rec(P, d, h, p, 1, 0, (int)rp, scx[0], scy[0], nzs[0][0], nzs[0][0], 0.0, 0.0);
 }
 
 // ---------------------------------------------------------------- stamps
@@ -1191,8 +1250,7 @@ __device__ __forceinline__ void wave_sync() {
 //  * step 4 (1691-1732): each ligand-free cis partner is snapped onto its
 //    unique ligand-bound partner.
 // Every value is computed by the same expressions as the one-lane version
-// (complex_align), so the result is bit-identical.  Requires csize <= 64 and
-// 3 * csize <= 64 (CXL).
+// (complex_align), so the result is bit-identical.  Requires csize <= 64 (CXL).
 
 // one random_shuffle pass over res[0 .. size-2] (libstdc++, main.cpp:1285)
 // on the row held one member per lane
@@ -1220,13 +1278,20 @@ __device__ __forceinline__ void wave_publish_row(const CX& X, CxLds* L, int v, i
   wave_sync();
 }
 
+// Lane t stands for member t (BFS position); its encoded protein number
+// (CxLds: receptor t -> t, ligand t -> NA + t) is t only for a receptor, so
+// the receptor steps take the lanes whose member is a receptor
+__device__ __forceinline__ bool lane_receptor(const CxLds* L, int csize, int NA, int lane) {
+  return lane < csize && L->slot[lane] < NA;
+}
+
 // steps 0 and 3: receptor m onto its ligand site
 template <class CX>
-__device__ __forceinline__ void wave_snap_bonds(const CX& X, int lane) {
+__device__ __forceinline__ void wave_snap_bonds(const CX& X, const CxLds* L, int lane) {
   const KParams& P = X.P;
   const int NA = P.NA;
   const int m = lane;
-  if (m < X.size && m < NA && X.neiA2(m) != 0) {
+  if (lane_receptor(L, X.size, NA, lane) && X.neiA2(m) != 0) {
     int lb = X.neiA2(m) - 1 - NA, j = X.neiA4(m);
     if (bond_misaligned(P, X.N, lb, j, m)) {
       X.set_moved(m);
@@ -1252,25 +1317,29 @@ __device__ __forceinline__ bool step2_fires(const CX& X, int B, int j, int& a1) 
 }
 
 // the first (member position, site) at or after candidate c0 (c = csi * 3 +
-// j - 2) whose test fires, or -1; its receptor in a1 (uniform)
+// j - 2) whose test fires, or -1; its receptor in a1 (uniform).  64
+// candidates per ballot, from the chunk holding c0.
 template <class CX>
 __device__ __forceinline__ int step2_first(const CX& X, int v, int c0, int lane, int& a1) {
-  const int c = lane, csi = c / 3, j = 2 + c % 3;
-  const int B = __shfl(v, min(csi, 63), 64);
-  int my_a1 = 0;
-  const bool f = c >= c0 && c < 3 * X.size && step2_fires(X, B, j, my_a1);
-  const uint64_t m = __ballot(f);
-  if (!m) return -1;
-  const int first = __ffsll((unsigned long long)m) - 1;
-  a1 = __shfl(my_a1, first, 64);
-  return first;
+  for (int base = c0 & ~63; base < 3 * X.size; base += 64) {
+    const int c = base + lane, csi = c / 3, j = 2 + c % 3;
+    const int B = __shfl(v, min(csi, 63), 64);
+    int my_a1 = 0;
+    const bool f = c >= c0 && c < 3 * X.size && step2_fires(X, B, j, my_a1);
+    const uint64_t m = __ballot(f);
+    if (!m) continue;
+    const int first = __ffsll((unsigned long long)m) - 1;
+    a1 = __shfl(my_a1, first, 64);
+    return base + first;
+  }
+  return -1;
 }
 
 // lable4's body at candidate c: the ligand re-laid one bead per lane, then
 // lane 0 snaps its receptors and their partners (main.cpp:1441-1583)
 template <class CX>
 __device__ __forceinline__ void wave_step2_body(const CX& X, int v, int c, int a1, int lane) {
-  const int B = __shfl(v, c / 3, 64), j = 2 + c % 3;
+  const int B = __shfl(v, min(c / 3, 63), 64), j = 2 + c % 3;
   if (lane < 8) step2_relayout(X, B, j, a1, lane);
   if (lane == 0) X.set_moved(B);
   wave_sync();
@@ -1288,7 +1357,7 @@ __device__ __forceinline__ void multi_ligand_align_wave(const CX& X, CxLds* L, i
   int v = lane < csize ? X.res[lane] : 0;  // the row, one member per lane
   // step 0
   v = wave_shuffle(X, v, call++, lane);
-  wave_snap_bonds(X, lane);
+  wave_snap_bonds(X, L, lane);
   // step 1: moved flags as left by step 0, read before any is set
   v = wave_shuffle(X, v, call++, lane);
   wave_publish_row(X, L, v, lane);
@@ -1296,7 +1365,7 @@ __device__ __forceinline__ void multi_ligand_align_wave(const CX& X, CxLds* L, i
     const int pa = lane;
     bool go = false;
     int a2 = 0;
-    if (pa < csize && pa < NA && X.neiA2(pa) != 0 && X.neiA3(pa) != 0 && X.rnei(X.neiA3(pa), 2) != 0 &&
+    if (lane_receptor(L, csize, NA, lane) && X.neiA2(pa) != 0 && X.neiA3(pa) != 0 && X.rnei(X.neiA3(pa), 2) != 0 &&
         !X.is_moved(pa)) {
       a2 = X.neiA3(pa) - 1;
       go = X.is_moved(a2) || L->pos[pa] < L->pos[a2];  // the partner does not come first
@@ -1336,11 +1405,11 @@ __device__ __forceinline__ void multi_ligand_align_wave(const CX& X, CxLds* L, i
   }
   wave_publish_row(X, L, v, lane);
   // step 3
-  wave_snap_bonds(X, lane);
+  wave_snap_bonds(X, L, lane);
   // step 4
   {
     const int m = lane;
-    if (m < csize && m < NA && X.neiA2(m) != 0 && X.neiA3(m) != 0 && X.rnei(X.neiA3(m), 2) == 0) {
+    if (lane_receptor(L, csize, NA, lane) && X.neiA2(m) != 0 && X.neiA3(m) != 0 && X.rnei(X.neiA3(m), 2) == 0) {
       int a2 = X.neiA3(m) - 1;
       if (cis_misaligned(P, N, m, a2)) snap_cis(P, N, a2, m, P.cis_cut);
     }
@@ -1505,27 +1574,31 @@ __device__ __forceinline__ void cx_write_back(const Dev& d, CxLds* L, int* grow,
   }
 }
 
-// the old record of member m (lane < csize): its rank in its cell
-__device__ __forceinline__ int cx_count_old(const KParams& P, const Dev& d, int m) {
-  double x, y, zl, zh;
-  ref_point(d, d.cur, m, P.NA, x, y, zl, zh);
-  return atomicAdd(&d.cell_cnt[rec_cell(P, x, y, m >= P.NA)], 1);
-}
-// the staged members' new records (reference point from LDS); rk_old < 0:
-// count the old one here too
-__device__ __forceinline__ void cx_count(const KParams& P, const Dev& d, CxLds* L, int csize, int lane, int rk_old = -1) {
+// the staged members' new records (reference point from LDS; the old ones
+// were written by k_move_members), and the extent bound of the proposals
+__device__ __forceinline__ void cx_put_new(const KParams& P, const Dev& d, CxLds* L, int csize, int lane, int own) {
   if (lane >= csize) return;
   const int m = L->slot[lane];
   const double* b = L->bead[lane];
   const int kind = m >= P.NA;
-  if (rk_old < 0) rk_old = cx_count_old(P, d, m);
   bool ext = true;
   for (int j = 2; j <= 4; ++j) {
     const int o = (kind ? (j - 1) * 2 : (j - 1) * 4) * 3;
     const double ex = b[o] - b[0], ey = b[o + 1] - b[1];
     ext &= kind ? ex * ex + ey * ey <= 35.0 * 35.0 : ex * ex + ey * ey <= 0.09;
   }
-  count_new(P, d, m, rk_old, b[0], b[1], ext);
+  if (!ext) atomicOr(&d.ctl->err, ERR_GEOMETRY);
+  // reference point (ref_point): [1][1] xy; z span of the domain centres
+  // [j][1] (receptor) or the centre's z (ligand); receptor [3][3] site
+  double zl = b[2], zh = b[2], sx = 0.0, sy = 0.0;
+  if (!kind) {
+    const double z1 = b[2], z2 = b[(4) * 3 + 2], z3 = b[(8) * 3 + 2], z4 = b[(12) * 3 + 2];
+    zl = fmin(fmin(z1, z2), fmin(z3, z4));
+    zh = fmax(fmax(z1, z2), fmax(z3, z4));
+    sx = b[(2 * 4 + 2) * 3];
+    sy = b[(2 * 4 + 2) * 3 + 1];
+  }
+  put_rec(P, d, d.home[m], m, 1, rec_status(P, d, m), own, b[0], b[1], zl, zh, sx, sy);
 }
 
 // Rigid move of one complex, main.cpp:974-1131.  Lane = (member ql of a pass
@@ -1763,7 +1836,20 @@ __device__ __forceinline__ void move_member(const KParams& P, const Dev& d, int 
   for (int a = 0; a < 3; ++a)
 #pragma unroll
     for (int b = 0; b < 3; ++b) t.t[a][b] = cp[7 + a * 3 + b];
-  d.rank[p].x = atomicAdd(&d.cell_cnt[rec_cell(P, r[0].x, r[0].y, IS_A ? 0 : 1)], 1);
+  // both records (the new one is rewritten by k_complex_heavy when the
+  // complex's lay-down / alignment changes beads): reference point [1][1]
+  // (row 0), z span of the domain centres (rows 16, 20: z of [1..4][1]) or the
+  // ligand centre's z (row 8), receptor [3][3] site (row 10)
+  const uint2 h = d.home[p];
+  const int st = rec_status(P, d, p), own = d.owner[p];
+  auto recs = [&](int w) {
+    if constexpr (IS_A)
+      put_rec(P, d, h, p, w, st, own, r[0].x, r[0].y, fmin(fmin(r[16].x, r[16].y), fmin(r[20].x, r[20].y)),
+              fmax(fmax(r[16].x, r[16].y), fmax(r[20].x, r[20].y)), r[10].x, r[10].y);
+    else
+      put_rec(P, d, h, p, w, st, own, r[0].x, r[0].y, r[8].x, r[8].x, 0.0, 0.0);
+  };
+  recs(0);
   // beads (j, k) and (j+1, k), j odd: xy rows (j-1)·NK + (k-1) and j·NK + (k-1),
   // their z pair in row 4·NK + ((j-1)>>1)·NK + (k-1); moved in place
 #pragma unroll
@@ -1780,6 +1866,7 @@ __device__ __forceinline__ void move_member(const KParams& P, const Dev& d, int 
     }
 #pragma unroll
   for (int w = 0; w < ROWS; ++w) st_n(dst[(size_t)w * n + i], r[w]);
+  recs(1);
 }
 
 __global__ void __launch_bounds__(256) k_cx_check(KParams P, Dev d) {
@@ -1808,7 +1895,7 @@ __global__ void __launch_bounds__(256) k_cx_check(KParams P, Dev d) {
       continue;
     }
     const int* row = d.members + desc.y;
-    for (int t = 0; t < csize; ++t) {  // the members' new records
+    for (int t = 0; t < csize; ++t) {  // the extent bound of the members' proposals (records: k_move_members)
       const int m = row[t];
       const bool isA = m < NA;
       double2 b[4];
@@ -1820,7 +1907,7 @@ __global__ void __launch_bounds__(256) k_cx_check(KParams P, Dev d) {
         const double ex = b[j].x - b[0].x, ey = b[j].y - b[0].y;
         ext &= isA ? ex * ex + ey * ey <= 0.09 : ex * ex + ey * ey <= 35.0 * 35.0;
       }
-      count_new(P, d, m, d.rank[m].x, b[0].x, b[0].y, ext);
+      if (!ext) atomicOr(&d.ctl->err, ERR_GEOMETRY);
     }
   }
 }
@@ -1855,7 +1942,7 @@ __global__ void __launch_bounds__(256) k_complex_heavy(KParams P, Dev d) {
       complex_align(X, nB, lb, pA);
     }
     wave_sync();
-    for (int q = lane; q < csize; q += 64) count_records(P, d, grow[q]);
+    for (int q = lane; q < csize; q += 64) put_recs_glb(P, d, grow[q]);
   };
   if (blockIdx.x == 0 && threadIdx.x < 64) {
     const uint32_t no = d.ctl->n_overflow;
@@ -1899,11 +1986,16 @@ __global__ void __launch_bounds__(256) k_complex_heavy(KParams P, Dev d) {
       const int pA = rm ? 63 - __clzll((long long)rm) : -1;
       CxT<LdsBeads, LdsLinks> X{P, step, (uint32_t)desc.w, L->res, csize, LdsBeads{L}, LdsLinks{L, NA}, &d.ctl->err,
                                 L->rnd};
-      complex_align_wave(X, L, nB, pA, lane);  // the root is member 0
+      if (P.cx_serial) {  // debug (KMC_CX_SERIAL=1): the one-lane alignment
+        if (lane == 0) complex_align(X, nB, 0, pA);
+        wave_sync();
+      } else {
+        complex_align_wave(X, L, nB, pA, lane);  // the root is member 0
+      }
     }
     cx_write_back(d, L, d.shuf + desc.y, csize, nB, NA, lane);  // shuffled row: shuf (members keeps BFS order)
     if (nB > 1 && lane == 0) d.shuf_tag[lb] = step;
-    cx_count(P, d, L, csize, lane, lane < csize ? d.rank[L->slot[lane]].x : 0);  // old rank: k_move_members
+    cx_put_new(P, d, L, csize, lane, desc.w);
     wave_sync();
   }
 }
@@ -1919,8 +2011,8 @@ __device__ __forceinline__ void propose_one(const KParams& P, const Dev& d, int 
   } else if (k == U_DIMER) {
     const int q = A_NEI3(d, p) - 1;
     propose_dimer(P, d, p, q, step);
-    count_records(P, d, p);
-    count_records(P, d, q);
+    put_recs_glb(P, d, p);
+    put_recs_glb(P, d, q);
   } else if (k == U_FREE_B) {
     propose_free_b(P, d, p - P.NA, p, step);
   }
@@ -1948,55 +2040,6 @@ __global__ void __launch_bounds__(256) k_propose_free(KParams P, Dev d, int gC) 
     return;
   }
   propose_one(P, d, (int)((blockIdx.x - gC) * blockDim.x + threadIdx.x));
-}
-
-#define RID_PID 0x00ffffff
-#define RID_FIN (1 << 24)  // record holds its protein's final position (new: set by the scatter; moved to
-                           // the old record by k_rej_commit for rejected units)
-#define RID_ST3 (1 << 29)
-#define RID_ST2 (1 << 30)
-__global__ void k_rec_scatter(KParams P, Dev d) {
-  const int NA = P.NA;
-  int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= P.N) return;
-  int st = 0;
-  if (p < NA) st = (A_ST2(d, p) ? RID_ST2 : 0) | (A_ST3(d, p) ? RID_ST3 : 0);
-  const int2 rk = d.rank[p];
-  const int own = d.owner[p];
-  // both records' loads are issued before either store (two independent
-  // load -> cell -> cell_start chains in flight per lane)
-  double x[2], y[2], zl[2], zh[2];
-  float2 site[2];
-  int pos[2], end[2];
-#pragma unroll
-  for (int w = 0; w < 2; ++w) {
-    const Beads& B = w ? d.nxt : d.cur;
-    ref_point(d, B, p, NA, x[w], y[w], zl[w], zh[w]);
-    if (p < NA) {
-      const double2 s33 = B.Axy(p, 3, 3);
-      site[w] = make_float2((float)s33.x, (float)s33.y);
-    } else {
-      site[w] = make_float2(0.f, 0.f);
-    }
-  }
-#pragma unroll
-  for (int w = 0; w < 2; ++w) {
-    const int c = rec_cell(P, x[w], y[w], p >= NA);
-    pos[w] = d.cell_start[c] + (w ? rk.y : rk.x);
-    end[w] = d.cell_start[c + 1];
-  }
-#pragma unroll
-  for (int w = 0; w < 2; ++w) {
-    if ((w ? rk.y : rk.x) < 0 || pos[w] >= end[w]) {  // a protein no unit counted: inconsistent bond graph
-      atomicOr(&d.ctl->err, ERR_RESOLVE);
-      continue;
-    }
-    Rec rc;
-    rc.pos = make_float4((float)x[w], (float)y[w], (float)zl[w], (float)zh[w]);
-    rc.id = make_int2(p | st | (w << 31) | (w ? RID_FIN : 0), own);
-    rc.site = site[w];
-    d.rec[pos[w]] = rc;  // one 32-byte store
-  }
 }
 
 // ================================================================ 4. resolve
@@ -2204,107 +2247,244 @@ __device__ __forceinline__ void wg_flush(WgList& L, const SList& out, uint32_t* 
 }
 
 // ---------------------------------------------------------------- LDS tiles
-// Records are sorted by (cell row, kind, cell column) — cell_index() — so the
-// records of one kind in a run of columns of one row are contiguous.
-//
 // A workgroup owns a tile×tile block of cells (tile chosen on the host from
-// the record density).  It stages the records of the block plus a one-cell
-// halo into LDS as 2·halo segments (one per halo row and kind; each one
-// contiguous range of the sorted array, all loads in flight at once) and tags
-// every staged record with its (segment, column).  Every scanning record of
-// the block then takes the LDS indices of the records in its cut stencil —
-// per neighbour kind, only the cells within that kind pair's reach of the
-// record (its offset inside its cell decides which side columns / rows can
-// hold a partner) — as six LDS index ranges, and each wave walks its records'
-// pairs with every lane busy (tile_walk).
+// the record density).  It stages into LDS every record whose cell lies in
+// the block or its one-cell halo: those are the records of the home cells of
+// the block + two cells (home list, §records) whose cell code puts them into
+// the halo region, plus the outliers listed this step that fall into it.
+// The home cells of a (row, kind) run of columns are one contiguous range of
+// the home list, so the staging reads 2·(tile + 4) contiguous ranges, all in
+// flight at once.  The staged records are binned by their cell in LDS
+// (counting sort: LDS atomics, one block scan, scatter) and tagged with
+// (segment = halo row · 2 + kind, column).  Every scanning record of the
+// block then takes the LDS indices of the records in its cut stencil — per
+// neighbour kind, only the cells within that kind pair's reach of the record
+// (its offset inside its cell decides which side columns / rows can hold a
+// partner) — as six LDS index ranges, and each wave walks its records' pairs
+// with every lane busy (tile_walk).
 #ifndef TILE_MAX  // (overridable for tile-size sweeps: tools/build_variants.py)
 #define TILE_MAX 14
 #endif
 #define HALO_MAX (TILE_MAX + 2)
 #define NSEG_MAX (2 * HALO_MAX)
+#define HOME_MAX (TILE_MAX + 4)
+#define HSEG_MAX (2 * HOME_MAX)
+#define CFLAT_MAX (NSEG_MAX * (HALO_MAX + 1) + 1)
 #ifndef TCAP
 #define TCAP 768
 #endif
 struct TileLds {
   float4 pos[TCAP];
   int2 id[TCAP];
+  int gidx[TCAP];                      // global record index of each staged record
   uint16_t tag[TCAP];                  // segment | column << 8 of each staged record
-  int cstart[NSEG_MAX][HALO_MAX + 1];  // segment = halo row * 2 + kind: LDS index of each cell's first record; [seg][halo] = end
-  int goff[NSEG_MAX];                  // global record index − LDS index, per segment
-  int n;
+  int cstart[CFLAT_MAX];               // [seg][halo + 1] flat: record counts, then the LDS index of each cell's
+                                       // first record; [seg][halo] = the segment's end
+  int hs[HSEG_MAX][HOME_MAX + 1];      // home segment = home row * 2 + kind: first home position of each column
+  int hoff[HSEG_MAX + 1];              // home entries before each home segment; [nhseg] = total
+  int n, nseq;
 };
+__device__ __forceinline__ int& tcs(TileLds& T, int halo, int seg, int hx) { return T.cstart[seg * (halo + 1) + hx]; }
+__device__ __forceinline__ int tcs(const TileLds& T, int halo, int seg, int hx) { return T.cstart[seg * (halo + 1) + hx]; }
 
-__device__ __forceinline__ int cell_index(const KParams& P, int cx, int cy, int kind) {
-  return (cy * 2 + kind) * P.ncx + cx;
+__device__ __forceinline__ int tile_global(const TileLds& T, int l) { return T.gidx[l]; }
+
+// exclusive prefix sum of a[0..m) in LDS by the whole workgroup (m <= 4·blockDim)
+__device__ __forceinline__ int block_excl_scan(int* a, int m, int* wtot) {
+  const int t = threadIdx.x, lane = __lane_id(), w = t >> 6, nw = blockDim.x >> 6;
+  int v[4], sum = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int i = 4 * t + k;
+    v[k] = i < m ? a[i] : 0;
+    sum += v[k];
+  }
+  int inc = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += u;
+  }
+  if (lane == 63) wtot[w] = inc;
+  __syncthreads();
+  int base = 0, tot = 0;
+  for (int k = 0; k < nw; ++k) {
+    base += k < w ? wtot[k] : 0;
+    tot += wtot[k];
+  }
+  int run = base + inc - sum;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int i = 4 * t + k;
+    if (i < m) a[i] = run;
+    run += v[k];
+  }
+  __syncthreads();
+  return tot;
 }
 
-__device__ __forceinline__ int tile_global(const TileLds& T, int l) { return l + T.goff[T.tag[l] & 0xff]; }
+// Element q of a tile's staging sequence: the home records (2 per home entry,
+// segment by segment) then the outlier list.  Returns the global record index
+// and the record's cell (absolute), or -1 when the element holds no record of
+// the halo region (an outlier listed elsewhere, or a record beyond the halo).
+struct TileGeo {
+  int cx0, cy0, halo, hx0, hy0, nhseg, home;
+};
+__device__ __forceinline__ int tile_elem(const KParams& P, const Dev& d, const TileLds& T, const TileGeo& G, int q,
+                                         int& ax, int& ay, int& kind) {
+  const int nrec = 2 * T.hoff[G.nhseg];
+  if (q < nrec) {
+    const int e = q >> 1, w = q & 1;
+    int seg = 0;  // last segment with hoff <= e
+#pragma unroll
+    for (int st = 32; st; st >>= 1)
+      if (seg + st <= G.nhseg - 1 && T.hoff[seg + st] <= e) seg += st;
+    const int hp = T.hs[seg][0] + (e - T.hoff[seg]);
+    int hx = 0;  // last column whose first home position is <= hp
+#pragma unroll
+    for (int st = 16; st; st >>= 1)
+      if (hx + st <= G.home - 1 && T.hs[seg][hx + st] <= hp) hx += st;
+    ax = G.hx0 + hx;
+    ay = G.hy0 + (seg >> 1);
+    kind = seg & 1;
+    return 2 * hp + w;
+  }
+  const int4 o = d.outl[q - nrec];
+  ax = o.y;
+  ay = o.z;
+  kind = -1;  // from the record
+  return o.x;
+}
 
-// Returns false (uniformly) when the tile holds more than P.tcap records; the
-// caller then takes the global-memory path.  site (reaction scan only): the
-// [3][3] site of each record; its final flag goes into id.x as RID_FIN.
-__device__ bool tile_load(const KParams& P, const Dev& d, int tx, int ty, TileLds& T, float2* site, uint32_t step,
-                          Stamper& S) {
-  const int tile = P.tile, halo = tile + 2, nseg = 2 * halo;
-  const int cx0 = tx * tile - 1, cy0 = ty * tile - 1;
-  const int xlo = max(cx0, 0), xhi = min(cx0 + halo - 1, P.ncx - 1);
-  for (int idx = threadIdx.x; idx < nseg * (halo + 1); idx += blockDim.x) {
-    int seg = idx / (halo + 1), hx = idx - seg * (halo + 1);
-    int y = cy0 + (seg >> 1);
-    int v = 0;
-    if (y >= 0 && y < P.ncy && xlo <= xhi) {
-      int x = min(max(cx0 + hx, xlo), xhi + 1);
-      v = d.cell_start[cell_index(P, x, y, seg & 1)];
+// Stage the tile's records.  Returns false (uniformly) when more than P.tcap
+// records fall into the block + halo; the caller then takes the brute-force
+// global-memory path.
+__device__ bool tile_load(const KParams& P, const Dev& d, int tx, int ty, TileLds& T, float2* site, Stamper& S,
+                          TileGeo& G) {
+  const int tile = P.tile, halo = tile + 2, nseg = 2 * halo, home = tile + 4, nhseg = 2 * home;
+  G.halo = halo;
+  G.home = home;
+  G.nhseg = nhseg;
+  G.cx0 = tx * tile - 1;
+  G.cy0 = ty * tile - 1;
+  G.hx0 = G.cx0 - 1;
+  G.hy0 = G.cy0 - 1;
+  const int nflat = nseg * (halo + 1) + 1;
+  __shared__ int wtot[16];
+  {  // home segment heads; cell counters zeroed
+    const int xlo = max(G.hx0, 0), xhi = min(G.hx0 + home - 1, P.ncx - 1);
+    for (int idx = threadIdx.x; idx < nhseg * (home + 1); idx += blockDim.x) {
+      const int seg = idx / (home + 1), hx = idx - seg * (home + 1);
+      const int y = G.hy0 + (seg >> 1);
+      int v = 0;
+      if (y >= 0 && y < P.ncy && xlo <= xhi) v = d.hstart[cell_index(P, min(max(G.hx0 + hx, xlo), xhi + 1), y, seg & 1)];
+      T.hs[seg][hx] = v;
     }
-    T.cstart[seg][hx] = v;
+    for (int idx = threadIdx.x; idx < nflat; idx += blockDim.x) T.cstart[idx] = 0;
   }
   __syncthreads();
   S(d, 0);
-  if (threadIdx.x < 64) {  // segment lengths -> LDS segment bases (wave-0 inclusive scan)
-    int seg = threadIdx.x;
-    int len = seg < nseg ? T.cstart[seg][halo] - T.cstart[seg][0] : 0;
+  if (threadIdx.x < 64) {  // home segment lengths -> entries before each segment
+    const int seg = threadIdx.x;
+    const int len = seg < nhseg ? T.hs[seg][home] - T.hs[seg][0] : 0;
     int inc = len;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-      int t = __shfl_up(inc, o, 64);
+      const int t = __shfl_up(inc, o, 64);
       if (seg >= o) inc += t;
     }
-    if (seg < nseg) T.goff[seg] = T.cstart[seg][0] - (inc - len);
-    if (seg == nseg - 1) T.n = inc;
+    const int total = __shfl(inc, 63, 64);
+    if (seg <= nhseg) T.hoff[seg] = inc - len;
+    if (seg == 0) T.nseq = 2 * total + (int)min(d.ctl->n_outl, d.outl_cap);
   }
   __syncthreads();
   S(d, 1);
-  for (int idx = threadIdx.x; idx < nseg * (halo + 1); idx += blockDim.x) {
-    int seg = idx / (halo + 1), hx = idx - seg * (halo + 1);
-    T.cstart[seg][hx] -= T.goff[seg];
+  const int nseq = T.nseq;
+  const bool one = nseq <= 4 * (int)blockDim.x;  // every element held in registers through the binning
+  Rec rr[4];
+  int cell[4], rank[4], gi[4];
+  // elements base + k·blockDim + tid (four in flight per thread): record,
+  // global index, flat cell index (-1: not in the block + halo)
+  auto fetch = [&](int base) {
+    int ax[4], ay[4], kd[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int q = base + k * (int)blockDim.x + (int)threadIdx.x;
+      gi[k] = q < nseq ? tile_elem(P, d, T, G, q, ax[k], ay[k], kd[k]) : -1;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (gi[k] >= 0) rr[k] = d.rec[gi[k]];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      cell[k] = -1;
+      if (gi[k] < 0) continue;
+      int x = ax[k], y = ay[k];
+      if (kd[k] >= 0) {  // home record: its cell from the code; outliers come from the list
+        const int c = rec_code(rr[k].id);
+        if (c == RID_OUT) continue;
+        x += c % 3 - 1;
+        y += c / 3 - 1;
+      }
+      const int hx = x - G.cx0, hy = y - G.cy0;
+      if (hx < 0 || hx >= halo || hy < 0 || hy >= halo) continue;
+      const int kind = (rr[k].id.x & RID_PID) >= P.NA;
+      cell[k] = (hy * 2 + kind) * (halo + 1) + hx;
+    }
+  };
+  auto count = [&]() {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (cell[k] >= 0) rank[k] = atomicAdd(&T.cstart[cell[k]], 1);
+  };
+  if (one) {
+    fetch(0);
+    count();
+  } else {
+    for (int base = 0; base < nseq; base += 4 * blockDim.x) {
+      fetch(base);
+      count();
+    }
   }
   __syncthreads();
   S(d, 2);
-  const int n = T.n;
-  if (n > P.tcap) return false;
-  for (int idx = threadIdx.x; idx < nseg * halo; idx += blockDim.x) {  // tags: one thread per cell
-    int seg = idx / halo, hx = idx - seg * halo;
-    for (int l = T.cstart[seg][hx]; l < T.cstart[seg][hx + 1]; ++l) T.tag[l] = (uint16_t)(seg | hx << 8);
-  }
-  __syncthreads();
+  const int n = block_excl_scan(T.cstart, nflat, wtot);
+  if (threadIdx.x == 0) T.n = n;
   S(d, 3);
-  // four records per thread in flight: loads from clamped indices first, then
-  // the LDS stores (keeps the staging arrays in registers)
-  for (int base = 0; base < n; base += 4 * blockDim.x) {
-    Rec rc[4];
+  if (n > P.tcap) return false;
+  auto place = [&](int k, int l, int g) {
+    T.pos[l] = rr[k].pos;
+    T.id[l] = rr[k].id;
+    T.gidx[l] = g;
+    if (site) site[l] = rr[k].site;
+    const int c = cell[k], seg = c / (halo + 1), hx = c - seg * (halo + 1);
+    T.tag[l] = (uint16_t)(seg | hx << 8);
+  };
+  if (one) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      int l = min(base + k * (int)blockDim.x + (int)threadIdx.x, n - 1);
-      rc[k] = d.rec[tile_global(T, l)];
+    for (int k = 0; k < 4; ++k)
+      if (cell[k] >= 0) place(k, T.cstart[cell[k]] + rank[k], gi[k]);
+  } else {
+    // a second pass with the counters as cursors: each ends at its cell's
+    // end (= the next cell's start), shifted back afterwards
+    for (int base = 0; base < nseq; base += 4 * blockDim.x) {
+      fetch(base);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (cell[k] >= 0) place(k, atomicAdd(&T.cstart[cell[k]], 1), gi[k]);
     }
+    __syncthreads();
+    int v[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      int l = base + k * (int)blockDim.x + (int)threadIdx.x;
-      if (l < n) {
-        if (site) site[l] = rc[k].site;
-        T.pos[l] = rc[k].pos;
-        T.id[l] = rc[k].id;
-      }
+      const int i = 4 * (int)threadIdx.x + k;
+      v[k] = i >= 1 && i < nflat ? T.cstart[i - 1] : 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int i = 4 * (int)threadIdx.x + k;
+      if (i < nflat) T.cstart[i] = v[k];
     }
   }
   __syncthreads();
@@ -2326,8 +2506,8 @@ __device__ __forceinline__ void item_ranges(const KParams& P, const TileLds& T, 
   for (int k = 0; k < 3; ++k) {
     const int s = (hy - 1 + k) * 2 + kind;
     const bool on = k == 1 || (k == 0 ? down : up);
-    r0[k] = on ? T.cstart[s][lo] : 0;
-    r1[k] = on ? T.cstart[s][hi + 1] : 0;
+    r0[k] = on ? tcs(T, P.tile + 2, s, lo) : 0;
+    r1[k] = on ? tcs(T, P.tile + 2, s, hi + 1) : 0;
   }
 }
 
@@ -2427,18 +2607,6 @@ __device__ __forceinline__ void pair_flush(const PairBuf& b, WgList& L, const SL
   }
 }
 
-// global-memory path (dense tile): the full 3x3 record ranges of one kind
-__device__ __forceinline__ void cell_ranges(const KParams& P, const Dev& d, int x, int y, int kind, int* r0, int* r1) {
-  int x0 = max(x - 1, 0), x1 = min(x + 1, P.ncx - 1);
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    int yy = y - 1 + k;
-    bool ok = yy >= 0 && yy < P.ncy;
-    r0[k] = ok ? d.cell_start[cell_index(P, x0, yy, kind)] : 0;
-    r1[k] = ok ? d.cell_start[cell_index(P, x1 + 1, yy, kind)] : 0;
-  }
-}
-
 // reach (xy, Å) of the float prefilters per kind pair, + 1 Å for the float
 // cell bounds: receptor-receptor 42, receptor-ligand 86.5, ligand-ligand: any
 // collision has centres < 130 Å apart (DESIGN.md §cell list), i.e. all cells
@@ -2468,19 +2636,6 @@ __device__ __forceinline__ bool col_pair(int NA, int2 me, float4 mp, int2 id, fl
   const bool isnew = id.x < 0;
   const bool own_ok = kq == u ? isnew : (kq > u ? !isnew : true);
   return (q != m) & own_ok & prefilter(m < NA, mp.x, mp.y, mp.z, mp.w, q < NA, rp);
-}
-
-// one proposal record against three row ranges of records from global memory
-__device__ __forceinline__ void col_scan_glb(const KParams& P, const Dev& d, WgList& L, const int* r0, const int* r1,
-                                             int rs, int2 me, float4 mp) {
-#pragma unroll
-  for (int k = 0; k < 3; ++k)
-    for (int r = r0[k]; r < r1[k]; ++r) {
-      const int2 id = d.rec[r].id;
-      if (!col_pair(P.NA, me, mp, id, d.rec[r].pos)) continue;
-      if (id.y < 0) atomicOr(&d.ctl->err, ERR_RESOLVE);
-      else col_emit(d, L, rs, r);
-    }
 }
 
 // ---------------------------------------------------------------- 4b. exact
@@ -2610,21 +2765,8 @@ __global__ void __launch_bounds__(1024) k_col_tail(KParams P, Dev d, int round0)
 }
 
 // ================================================================ 5. commit
-// The members of every rejected unit: their final position is the old one.
-// The final flag (RID_FIN) of each member's two records moves from the
-// proposal record (set by k_rec_scatter) to the old one — the reaction scan
-// reads finality from the records — then R is copied to R_new.
-// Record w (0 old, 1 proposal) of member m: located from its position in R /
-// R_new (so before R_new is overwritten) and its rank in the cell.
-__device__ __forceinline__ void rej_flag(const KParams& P, const Dev& d, int m, int w) {
-  const int NA = P.NA;
-  const Beads& B = w ? d.nxt : d.cur;
-  const double x = B.P(m, 1, 1, 0), y = B.P(m, 1, 1, 1);
-  const int2 rk = d.rank[m];
-  const int pos = d.cell_start[rec_cell(P, x, y, m >= NA)] + (w ? rk.y : rk.x);
-  const int st = m < NA ? (A_ST2(d, m) ? RID_ST2 : 0) | (A_ST3(d, m) ? RID_ST3 : 0) : 0;
-  d.rec[pos].id.x = m | st | (w ? (int)0x80000000 : RID_FIN);
-}
+// The members of every rejected unit: their final position is the old one,
+// R is copied to R_new (main.cpp:666-674, 851-863, 1831-1860).
 // bead row `row` of member m: R_new = R
 __device__ __forceinline__ void rej_copy(const KParams& P, const Dev& d, int m, int row) {
   const bool a = m < P.NA;
@@ -2635,11 +2777,9 @@ __device__ __forceinline__ void rej_copy(const KParams& P, const Dev& d, int m, 
   dst[(size_t)row * n + i] = src[(size_t)row * n + i];
 }
 
-// One wave per rejected unit; its lanes take the (member, record) flag moves,
-// then the (member, bead row) copies, of all members at once, so a complex
-// costs the same few dependent loads as a single protein.  Every flag move of
-// the wave reads R_new before any of its copies writes it (program order, and
-// each move's store depends on its loads).
+// One wave per rejected unit; its lanes take the (member, bead row) copies of
+// all members at once, so a complex costs the same few dependent loads as a
+// single protein.
 __global__ void k_rej_commit(KParams P, Dev d) {
   const int NA = P.NA;
   __shared__ uint32_t pre[NSHARD + 1];
@@ -2658,7 +2798,6 @@ __global__ void k_rej_commit(KParams P, Dev d) {
       q = A_NEI3(d, sl) - 1;
     }
     auto member = [&](int k) { return kind == U_COMPLEX ? d.members[off + k] : (k ? q : sl); };
-    for (int e = lane; e < 2 * nm; e += 64) rej_flag(P, d, member(e >> 1), e & 1);
     for (int e = lane; e < nm * ROWS_A; e += 64) rej_copy(P, d, member(e / ROWS_A), e % ROWS_A);
   }
 }
@@ -2671,10 +2810,15 @@ __global__ void k_rej_commit(KParams P, Dev d) {
 // every record of such a receptor (old and proposed) with every record near
 // it, with conservative single-precision prefilters (R–L: ligand centre within
 // reach of the [3][2] site; cis: the two [3][3] sites within 16 Å).  Exactly
-// one of a protein's two records is final (RID_FIN, moved by k_rej_commit),
-// so of the up to four record combinations of a protein pair at most one is
-// final-final: k_rxn_exact keeps that one — the same pairs as a scan of the
-// final records.
+// one of a protein's two records is final — the proposal if its unit was
+// accepted, the old position if it was rejected (rec_final) — so of the up to
+// four record combinations of a protein pair at most one is final-final:
+// k_rxn_exact keeps that one — the same pairs as a scan of the final records.
+// the record holds its protein's final position: the proposal of an accepted
+// unit or the old position of a rejected one (owner key = the unit)
+__device__ __forceinline__ bool rec_final(const Dev& d, int2 id, uint32_t step) {
+  return (state_of(d, id.y, step) == S_REJ) == (id.x >= 0);
+}
 __device__ __forceinline__ void rxn_emit(const Dev& d, WgList& L, int a, int b) {
   wg_emit(L, make_int2(a, b), d.pairs, &d.ctl->err);
 }
@@ -2699,15 +2843,6 @@ __device__ __forceinline__ bool rxn_pair(int NA, int2 me, float4 mp, float2 ms, 
   return (q != i) & (rl_ok | cis_ok);
 }
 
-// one receptor record against three row ranges, records from global memory
-__device__ __forceinline__ void rxn_scan_glb(const KParams& P, const Dev& d, WgList& L, const int* r0, const int* r1,
-                                             int rs, int2 me, float4 mp, float2 ms) {
-#pragma unroll
-  for (int k = 0; k < 3; ++k)
-    for (int r = r0[k]; r < r1[k]; ++r)
-      if (rxn_pair(P.NA, me, mp, ms, d.rec[r].id, d.rec[r].pos, d.rec[r].site)) rxn_emit(d, L, rs, r);
-}
-
 // ---------------------------------------------------------------- pair scan
 // One staging of each tile for both pair searches of the step: collision
 // candidates of the proposal records (pass A, §4a) and reaction candidates of
@@ -2724,7 +2859,8 @@ __global__ void __launch_bounds__(256) k_pair_scan(KParams P, Dev d) {
   wg_list_init(Lc);
   wg_list_init(Lr);
   Stamper S(0);
-  if (tile_load(P, d, tx, ty, T, site, 0, S)) {
+  TileGeo G;
+  if (tile_load(P, d, tx, ty, T, site, S, G)) {
     if (P.dbg_stage == 1) return;
     PairBuf Bc, Br;
     Bc.n = 0;
@@ -2778,32 +2914,46 @@ __global__ void __launch_bounds__(256) k_pair_scan(KParams P, Dev d) {
     S(d, 7);
     return;
   }
-  // dense tile: one thread per interior cell, records from global memory
-  for (int c = threadIdx.x; c < P.tile * P.tile; c += blockDim.x) {
-    int x = tx * P.tile + c % P.tile, y = ty * P.tile + c / P.tile;
-    if (x >= P.ncx || y >= P.ncy) continue;
-    int ra[3], rb[3], sa[3], sb[3];
-    cell_ranges(P, d, x, y, 0, ra, sa);
-    cell_ranges(P, d, x, y, 1, rb, sb);
-    for (int kind = 0; kind < 2; ++kind) {
-      int s0 = d.cell_start[cell_index(P, x, y, kind)], s1 = d.cell_start[cell_index(P, x + 1, y, kind)];
-      for (int r = s0; r < s1; ++r) {
-        const int2 me = d.rec[r].id;
-        const float4 mp = d.rec[r].pos;
-        if (me.x < 0) {
-          if (me.y < 0) {
-            atomicOr(&d.ctl->err, ERR_RESOLVE);
-          } else {
-            col_scan_glb(P, d, Lc, ra, sa, r, me, mp);
-            col_scan_glb(P, d, Lc, rb, sb, r, me, mp);
-          }
-        }
-        if (rxn_item(NA, me)) {
-          const float2 ms = d.rec[r].site;
-          rxn_scan_glb(P, d, Lr, ra, sa, r, me, mp, ms);
-          rxn_scan_glb(P, d, Lr, rb, sb, r, me, mp, ms);
-        }
+  // dense tile (more than tcap records): every interior record of the
+  // staging sequence against every sequence record of its 3x3 cells, records
+  // from global memory (never at the benchmark densities; KMC_DEBUG_TCAP)
+  const int nseq = T.nseq;
+  auto elem = [&](int q, Rec& r, int& x, int& y) -> int {
+    int kd;
+    const int ri = tile_elem(P, d, T, G, q, x, y, kd);
+    if (ri < 0) return -1;
+    r = d.rec[ri];
+    if (kd >= 0) {
+      const int c = rec_code(r.id);
+      if (c == RID_OUT) return -1;
+      x += c % 3 - 1;
+      y += c / 3 - 1;
+    }
+    return ri;
+  };
+  for (int qi = threadIdx.x; qi < nseq; qi += blockDim.x) {
+    Rec mr;
+    int x, y;
+    const int ri = elem(qi, mr, x, y);
+    if (ri < 0 || x - G.cx0 < 1 || x - G.cx0 > P.tile || y - G.cy0 < 1 || y - G.cy0 > P.tile) continue;
+    const int2 me = mr.id;
+    bool prop = me.x < 0;
+    if (prop && me.y < 0) {
+      atomicOr(&d.ctl->err, ERR_RESOLVE);
+      prop = false;
+    }
+    const bool rx = rxn_item(NA, me);
+    if (!prop && !rx) continue;
+    for (int qn = 0; qn < nseq; ++qn) {
+      Rec o;
+      int ox, oy;
+      const int rn = elem(qn, o, ox, oy);
+      if (rn < 0 || abs(ox - x) > 1 || abs(oy - y) > 1) continue;
+      if (prop && col_pair(NA, me, mr.pos, o.id, o.pos)) {
+        if (o.id.y < 0) atomicOr(&d.ctl->err, ERR_RESOLVE);
+        else col_emit(d, Lc, ri, rn);
       }
+      if (rx && rxn_pair(NA, me, mr.pos, mr.site, o.id, o.pos, o.site)) rxn_emit(d, Lr, ri, rn);
     }
   }
   wg_flush(Lc, d.cand, &d.ctl->err);
@@ -2823,7 +2973,7 @@ __global__ void k_rxn_exact(KParams P, Dev d) {
   for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
     const int2 pr = sl_at(d.pairs, pre, t);
     const int2 ra = d.rec[pr.x].id, rb = d.rec[pr.y].id;
-    if (!(ra.x & rb.x & RID_FIN)) continue;  // not both final positions (see the pair scan)
+    if (!rec_final(d, ra, step) || !rec_final(d, rb, step)) continue;  // not both final positions (see the pair scan)
     const int i = ra.x & RID_PID, q = rb.x & RID_PID;
     if (q >= NA) {
       int lb = q - NA;
@@ -3149,9 +3299,6 @@ __global__ void __launch_bounds__(256) k_diss_observe(KParams P, Dev d) {
   __shared__ int red[4][6];
   int p = blockIdx.x * blockDim.x + threadIdx.x;
   int v[6] = {0, 0, 0, 0, 0, 0};  // rl mono cis tot_prot tot_clu max
-  // the next step's cell counters (its buffer was consumed by the previous
-  // step's scan): coalesced zeroing here instead of a scattered store per record
-  for (int c = p; c < d.ncnt; c += gridDim.x * blockDim.x) d.cell_cnt_alt[c] = 0;
   if (p < NA) {
     const int i = p;
     const uint32_t step = d.ctl->step;
@@ -3279,6 +3426,7 @@ __global__ void __launch_bounds__(256) k_finalize(KParams P, Dev d, double time_
   c->n_pqe = 0;
   c->n_rl = 0;
   c->n_cisc = 0;
+  c->n_outl = 0;
 }
 
 
@@ -3290,10 +3438,10 @@ __global__ void __launch_bounds__(256) k_finalize(KParams P, Dev d, double time_
 // simulation depends on the slot order: random streams, unit keys and the
 // reactions' greedy order use reference indices (id_of); bond fields hold
 // slot + 1 and are renumbered with the permutation.
+// row-major cell order, the order of the home list: the free units' record
+// writes (at their home positions) then run along the home list
 __device__ __forceinline__ uint32_t slot_key(const KParams& P, double x, double y) {
-  const int cx = cell_x(P, x), cy = cell_y(P, y), t = P.tile;
-  const int ntx = (P.ncx + t - 1) / t;
-  return ((uint32_t)((cy / t) * ntx + cx / t) * t + (uint32_t)(cy % t)) * t + (uint32_t)(cx % t);
+  return (uint32_t)cell_y(P, y) * (uint32_t)P.ncx + (uint32_t)cell_x(P, x);
 }
 
 // Sort key of slot s: (cell << 32) | unit.  With grouping, a protein takes
@@ -3321,6 +3469,27 @@ __global__ void k_slot_keys(KParams P, Dev d, uint64_t* keys, int32_t* vals, int
   const uint64_t tail = group == 2 && d.croot[s] >= 0 ? 1ull << 63 : 0ull;
   keys[s] = tail | (uint64_t)slot_key(P, x, y) << 32 | (uint32_t)(group ? own : 0);
   vals[s] = s < P.NA ? s : s - P.NA;
+}
+
+// ---------------------------------------------------------------- home list
+// Rebuilt with the slot order (and after a state is set or a chunk undone):
+// the home cell of slot p is the (row, kind, column) cell of its reference
+// point [1][1] in R; home positions are handed out cell by cell (counting
+// sort: count with ranks, scan = hstart, place).
+__global__ void k_home_count(KParams P, Dev d, int32_t* hcnt) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P.N) return;
+  const double2 xy = p < P.NA ? d.cur.Axy(p, 1, 1) : d.cur.Bxy(p - P.NA, 1, 1);
+  const int cx = cell_x(P, xy.x), cy = cell_y(P, xy.y);
+  const int r = atomicAdd(&hcnt[cell_index(P, cx, cy, p >= P.NA)], 1);
+  d.home[p] = make_uint2((uint32_t)r, (uint32_t)cx | (uint32_t)cy << 16);
+}
+__global__ void k_home_place(KParams P, Dev d) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P.N) return;
+  const uint2 h = d.home[p];
+  const int cx = (int)(h.y & 0xffffu), cy = (int)(h.y >> 16);
+  d.home[p].x = (uint32_t)d.hstart[cell_index(P, cx, cy, p >= P.NA)] + h.x;
 }
 
 // perm[s'] = old slot of new slot s' (sorted values, per kind); inverse map
