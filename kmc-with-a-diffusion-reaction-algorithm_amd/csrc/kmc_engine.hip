@@ -163,6 +163,7 @@ int alloc_lists(kmc_sim* s) {
   dfree(s, d.gi32);
   dfree(s, d.pq_ent);
   dfree(s, d.outl);
+  dfree(s, d.dense);
   uint32_t cap = (uint32_t)scale(pow2(std::max<uint32_t>(4096, std::min<uint32_t>(1u << 20, (uint32_t)N / 8 + 1))));
   d.cap_edges = pow2(cap);
   int rc = KMC_OK;
@@ -187,6 +188,9 @@ int alloc_lists(kmc_sim* s) {
   // densities between re-sorts (a protein drifts a few Å per step)
   d.outl_cap = (uint32_t)scale(std::max<uint64_t>(1024, N / 64));
   rc |= dalloc(s, &d.outl, d.outl_cap);
+  // pair-scan blocks too dense for LDS (KMC_DEBUG_TCAP; never at the benchmark densities)
+  d.dense_cap = (uint32_t)scale(1024);
+  rc |= dalloc(s, &d.dense, d.dense_cap);
   return rc;
 }
 
@@ -367,7 +371,9 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   {
     const double rho = (double)N * K.cs * K.cs / std::max(1.0, p->box_x * p->box_y);  // proteins per cell
     int t = TILE_MAX;
-    while (t > 4 && (t * t * rho > 205.0 || (t + 2) * (t + 2) * 2.0 * rho > 0.6 * TCAP)) --t;
+    // (a block whose records still overflow TCAP is split into quarters by
+    // k_pair_scan itself: the bound below keeps that rare)
+    while (t > 4 && (t * t * rho > 205.0 || (t + 2) * (t + 2) * 2.0 * rho > 0.75 * TCAP)) --t;
     const char* te = getenv("KMC_TILE");
     if (te && *te) t = std::max(2, std::min(TILE_MAX, atoi(te)));
     K.tile = t;
@@ -784,7 +790,8 @@ static int launch_step(kmc_sim* s, bool re_sort) {
   const int ntiles = ((K.ncx + K.tile - 1) / K.tile) * ((K.ncy + K.tile - 1) / K.tile);
   // collision candidates and reaction candidates, one staging of each tile
   TIMED(KI_PAIR_SCAN, (k_pair_scan<<<ntiles, 256, 0, st>>>(K, d)));
-  TIMED(KI_COL_EXACT, (k_col_exact<<<gX, T, 0, st>>>(K, d)));
+  // (at least 64 workgroups: k_col_exact also scans the dense blocks, one per workgroup)
+  TIMED(KI_COL_EXACT, (k_col_exact<<<std::max(gX, 64), T, 0, st>>>(K, d)));
   TIMED(KI_COL_ROUNDS, {
     k_col_round<<<gX, T, 0, st>>>(K, d, 0);
     k_col_units<<<gX, T, 0, st>>>(K, d, 0);

@@ -79,6 +79,8 @@ struct Dev {
   struct Rec* rec;      // [2N] records, home order; written by the kernels that move the protein
   int4* outl;           // [outl_cap] records more than one cell from their home cell: {record, cx, cy, -}
   uint32_t outl_cap;
+  int4* dense;          // [dense_cap] blocks of cells whose records overflow the pair scan's LDS: {x0, y0, w, h}
+  uint32_t dense_cap;
   SList cand;           // collision candidates (proposal record, other record)
   SList conf;           // conflict entries (u, kq | isnew<<31)
   SList plist;          // units with conflict entries (u, 0)
@@ -105,7 +107,8 @@ struct alignas(16) Rec {
   int2 id;      // {slot | cell code << 25 | st3 << 29 | st2 << 30 | isnew << 31, owner key}
   float2 site;  // receptor [3][3] site xy (reaction prefilter); 0 for ligands
 };
-#define RID_PID 0x00ffffff
+#define RID_PID 0x00ffffff  // the slot (global records) or the home position (the pair scan's LDS copies)
+#define RID_LIG (1 << 24)   // a ligand's record
 #define RID_CODE_SHIFT 25  // 4-bit cell code: (dy + 1) * 3 + (dx + 1), the record's cell relative to its home
                            // cell; RID_OUT: more than one cell away (the record is on the outlier list)
 #define RID_OUT 15
@@ -571,7 +574,7 @@ __device__ __forceinline__ void put_rec(const KParams& P, const Dev& d, uint2 h,
   }
   Rec r;
   r.pos = make_float4((float)x, (float)y, (float)zlo, (float)zhi);
-  r.id = make_int2(p | code << RID_CODE_SHIFT | st | (w << 31), own);
+  r.id = make_int2(p | (p >= P.NA ? RID_LIG : 0) | code << RID_CODE_SHIFT | st | (w << 31), own);
   r.site = make_float2((float)sx, (float)sy);
   d.rec[ri] = r;
 }
@@ -2247,21 +2250,25 @@ __device__ __forceinline__ void wg_flush(WgList& L, const SList& out, uint32_t* 
 }
 
 // ---------------------------------------------------------------- LDS tiles
-// A workgroup owns a tile×tile block of cells (tile chosen on the host from
-// the record density).  It stages into LDS every record whose cell lies in
-// the block or its one-cell halo: those are the records of the home cells of
-// the block + two cells (home list, §records) whose cell code puts them into
-// the halo region, plus the outliers listed this step that fall into it.
-// The home cells of a (row, kind) run of columns are one contiguous range of
-// the home list, so the staging reads 2·(tile + 4) contiguous ranges, all in
-// flight at once.  The staged records are binned by their cell in LDS
-// (counting sort: LDS atomics, one block scan, scatter) and tagged with
-// (segment = halo row · 2 + kind, column).  Every scanning record of the
+// A workgroup owns a block of cells (tile×tile, the tile side chosen on the
+// host from the record density).  It stages into LDS every record whose cell
+// lies in the block or its one-cell halo: those are the records of the home
+// cells of the block + two cells (home list, §records) whose cell code puts
+// them into the halo region, plus the outliers listed this step that fall
+// into it.  The home cells of a (row, kind) run of columns are one contiguous
+// range of the home list, so the staging reads 2·(rows + 4) contiguous
+// ranges, all in flight at once; each home entry's column comes from a tag
+// written per home cell (no search).  The staged records are binned by their
+// cell in LDS (counting sort: LDS atomics, one block scan, scatter) and tagged
+// with (segment = halo row · 2 + kind, column).  Every scanning record of the
 // block then takes the LDS indices of the records in its cut stencil — per
 // neighbour kind, only the cells within that kind pair's reach of the record
 // (its offset inside its cell decides which side columns / rows can hold a
 // partner) — as six LDS index ranges, and each wave walks its records' pairs
-// with every lane busy (tile_walk).
+// with every lane busy (tile_walk).  A block whose records do not fit in
+// TCAP is split into quarters (down to single cells), each staged the same
+// way; only a single cell that still does not fit takes the brute-force
+// global-memory path.
 #ifndef TILE_MAX  // (overridable for tile-size sweeps: tools/build_variants.py)
 #define TILE_MAX 14
 #endif
@@ -2271,23 +2278,53 @@ __device__ __forceinline__ void wg_flush(WgList& L, const SList& out, uint32_t* 
 #define HSEG_MAX (2 * HOME_MAX)
 #define CFLAT_MAX (NSEG_MAX * (HALO_MAX + 1) + 1)
 #ifndef TCAP
-#define TCAP 768
+#define TCAP 640
 #endif
+#define HTAG_MAX 640  // home entries tagged for the direct column lookup (more: binary search)
+
+// the staged block: cells [x0, x0 + w) × [y0, y0 + h); halo region origin
+// (cx0, cy0) = (x0 - 1, y0 - 1), size hw × hh; home region origin (hx0, hy0)
+// = (x0 - 2, y0 - 2), size mw × mh (2·mh home segments)
+struct TileGeo {
+  int x0, y0, w, h, cx0, cy0, hw, hh, hx0, hy0, mw, mh, nhseg;
+};
+__device__ __forceinline__ TileGeo tile_geo(int x0, int y0, int w, int h) {
+  TileGeo G;
+  G.x0 = x0;
+  G.y0 = y0;
+  G.w = w;
+  G.h = h;
+  G.cx0 = x0 - 1;
+  G.cy0 = y0 - 1;
+  G.hw = w + 2;
+  G.hh = h + 2;
+  G.hx0 = x0 - 2;
+  G.hy0 = y0 - 2;
+  G.mw = w + 4;
+  G.mh = h + 4;
+  G.nhseg = 2 * G.mh;
+  return G;
+}
+
 struct TileLds {
   float4 pos[TCAP];
-  int2 id[TCAP];
-  int gidx[TCAP];                      // global record index of each staged record
-  uint16_t tag[TCAP];                  // segment | column << 8 of each staged record
-  int cstart[CFLAT_MAX];               // [seg][halo + 1] flat: record counts, then the LDS index of each cell's
-                                       // first record; [seg][halo] = the segment's end
-  int hs[HSEG_MAX][HOME_MAX + 1];      // home segment = home row * 2 + kind: first home position of each column
-  int hoff[HSEG_MAX + 1];              // home entries before each home segment; [nhseg] = total
-  int n, nseq;
+  int2 id[TCAP];                   // {home position | the record's flags, owner key}
+  uint16_t tag[TCAP];              // segment | column << 8 of each staged record's cell
+  int cstart[CFLAT_MAX];           // [seg][hw + 1] flat: record counts, then the LDS index of each cell's
+                                   // first record; [seg][hw] = the segment's end
+  int hs[HSEG_MAX][HOME_MAX + 1];  // home segment = home row * 2 + kind: first home position of each column
+  int hbase[HSEG_MAX];             // home position − home entry index, per home segment
+  int hoff[HSEG_MAX + 1];          // home entries before each home segment; [nhseg] = all
+  uint16_t htag[HTAG_MAX];         // home segment | column << 8 of each home entry
+  int n, nseq, nhome;
 };
-__device__ __forceinline__ int& tcs(TileLds& T, int halo, int seg, int hx) { return T.cstart[seg * (halo + 1) + hx]; }
-__device__ __forceinline__ int tcs(const TileLds& T, int halo, int seg, int hx) { return T.cstart[seg * (halo + 1) + hx]; }
+__device__ __forceinline__ int tcs(const TileLds& T, int hw, int seg, int hx) { return T.cstart[seg * (hw + 1) + hx]; }
 
-__device__ __forceinline__ int tile_global(const TileLds& T, int l) { return T.gidx[l]; }
+// global record index of staged record l (record w of home position hp at 2·hp + w)
+__device__ __forceinline__ int tile_global(const TileLds& T, int l) {
+  const int x = T.id[l].x;
+  return 2 * (x & RID_PID) + (x < 0 ? 1 : 0);
+}
 
 // exclusive prefix sum of a[0..m) in LDS by the whole workgroup (m <= 4·blockDim)
 __device__ __forceinline__ int block_excl_scan(int* a, int m, int* wtot) {
@@ -2323,70 +2360,93 @@ __device__ __forceinline__ int block_excl_scan(int* a, int m, int* wtot) {
   return tot;
 }
 
-// Element q of a tile's staging sequence: the home records (2 per home entry,
-// segment by segment) then the outlier list.  Returns the global record index
-// and the record's cell (absolute), or -1 when the element holds no record of
-// the halo region (an outlier listed elsewhere, or a record beyond the halo).
-struct TileGeo {
-  int cx0, cy0, halo, hx0, hy0, nhseg, home;
-};
-__device__ __forceinline__ int tile_elem(const KParams& P, const Dev& d, const TileLds& T, const TileGeo& G, int q,
-                                         int& ax, int& ay, int& kind) {
-  const int nrec = 2 * T.hoff[G.nhseg];
-  if (q < nrec) {
+// Element q of a block's staging sequence: the home records (2 per home
+// entry, segment by segment) then the outlier list.  Returns the global
+// record index, with the home cell (home records, kind >= 0) or the record's
+// own cell (outliers, kind = -1).
+__device__ __forceinline__ int tile_elem(const Dev& d, const TileLds& T, const TileGeo& G, int q, int& ax, int& ay,
+                                         int& kind) {
+  const int nhome = T.nhome;
+  if (q < 2 * nhome) {
     const int e = q >> 1, w = q & 1;
-    int seg = 0;  // last segment with hoff <= e
+    int seg, hx;
+    if (nhome <= HTAG_MAX) {
+      const int tg = T.htag[e];
+      seg = tg & 0xff;
+      hx = tg >> 8;
+    } else {  // more home entries than tags: search the segment, then the column
+      seg = 0;
 #pragma unroll
-    for (int st = 32; st; st >>= 1)
-      if (seg + st <= G.nhseg - 1 && T.hoff[seg + st] <= e) seg += st;
-    const int hp = T.hs[seg][0] + (e - T.hoff[seg]);
-    int hx = 0;  // last column whose first home position is <= hp
+      for (int st = 32; st; st >>= 1)
+        if (seg + st <= G.nhseg - 1 && T.hoff[seg + st] <= e) seg += st;
+      const int hp = T.hbase[seg] + e;
+      hx = 0;
 #pragma unroll
-    for (int st = 16; st; st >>= 1)
-      if (hx + st <= G.home - 1 && T.hs[seg][hx + st] <= hp) hx += st;
+      for (int st = 16; st; st >>= 1)
+        if (hx + st <= G.mw - 1 && T.hs[seg][hx + st] <= hp) hx += st;
+    }
     ax = G.hx0 + hx;
     ay = G.hy0 + (seg >> 1);
     kind = seg & 1;
-    return 2 * hp + w;
+    return 2 * (T.hbase[seg] + e) + w;
   }
-  const int4 o = d.outl[q - nrec];
+  const int4 o = d.outl[q - 2 * nhome];
   ax = o.y;
   ay = o.z;
-  kind = -1;  // from the record
+  kind = -1;
   return o.x;
 }
 
-// Stage the tile's records.  Returns false (uniformly) when more than P.tcap
-// records fall into the block + halo; the caller then takes the brute-force
-// global-memory path.
-__device__ bool tile_load(const KParams& P, const Dev& d, int tx, int ty, TileLds& T, float2* site, Stamper& S,
-                          TileGeo& G) {
-  const int tile = P.tile, halo = tile + 2, nseg = 2 * halo, home = tile + 4, nhseg = 2 * home;
-  G.halo = halo;
-  G.home = home;
-  G.nhseg = nhseg;
-  G.cx0 = tx * tile - 1;
-  G.cy0 = ty * tile - 1;
-  G.hx0 = G.cx0 - 1;
-  G.hy0 = G.cy0 - 1;
-  const int nflat = nseg * (halo + 1) + 1;
+// Stage the block's records.  Returns false (uniformly) when more than P.tcap
+// records fall into the block + halo (the home headers and tags stay valid
+// for the brute-force path).
+__device__ bool tile_load(const KParams& P, const Dev& d, const TileGeo& G, TileLds& T, float2* site, Stamper& S) {
+  const int hw = G.hw, hh = G.hh, mw = G.mw, nhseg = G.nhseg;
+  const int nflat = 2 * hh * (hw + 1) + 1;
   __shared__ int wtot[16];
-  {  // home segment heads; cell counters zeroed
-    const int xlo = max(G.hx0, 0), xhi = min(G.hx0 + home - 1, P.ncx - 1);
-    for (int idx = threadIdx.x; idx < nhseg * (home + 1); idx += blockDim.x) {
-      const int seg = idx / (home + 1), hx = idx - seg * (home + 1);
+#ifndef HDR_WAVE
+  {  // home segment heads, every load in flight before the stores; cell counters zeroed
+    const int xlo = max(G.hx0, 0), xhi = min(G.hx0 + mw - 1, P.ncx - 1);
+    constexpr int NH = (HSEG_MAX * (HOME_MAX + 1) + 255) / 256;
+    int v[NH];
+#pragma unroll
+    for (int k = 0; k < NH; ++k) {
+      const int idx = threadIdx.x + k * (int)blockDim.x;
+      const int seg = idx / (mw + 1), hx = idx - seg * (mw + 1);
       const int y = G.hy0 + (seg >> 1);
-      int v = 0;
-      if (y >= 0 && y < P.ncy && xlo <= xhi) v = d.hstart[cell_index(P, min(max(G.hx0 + hx, xlo), xhi + 1), y, seg & 1)];
-      T.hs[seg][hx] = v;
+      v[k] = 0;
+      if (seg < nhseg && y >= 0 && y < P.ncy && xlo <= xhi)
+        v[k] = d.hstart[cell_index(P, min(max(G.hx0 + hx, xlo), xhi + 1), y, seg & 1)];
+    }
+#pragma unroll
+    for (int k = 0; k < NH; ++k) {
+      const int idx = threadIdx.x + k * (int)blockDim.x;
+      const int seg = idx / (mw + 1), hx = idx - seg * (mw + 1);
+      if (seg < nhseg) T.hs[seg][hx] = v[k];
     }
     for (int idx = threadIdx.x; idx < nflat; idx += blockDim.x) T.cstart[idx] = 0;
   }
+#else
+  const int lane = __lane_id(), wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  {  // home segment heads (a wave per segment, a lane per column); cell counters zeroed
+    const int xlo = max(G.hx0, 0), xhi = min(G.hx0 + mw - 1, P.ncx - 1);
+    for (int seg = wv; seg < nhseg; seg += nwv) {
+      const int y = G.hy0 + (seg >> 1);
+      if (lane <= mw) {
+        int v = 0;
+        if (y >= 0 && y < P.ncy && xlo <= xhi)
+          v = d.hstart[cell_index(P, min(max(G.hx0 + lane, xlo), xhi + 1), y, seg & 1)];
+        T.hs[seg][lane] = v;
+      }
+    }
+    for (int idx = threadIdx.x; idx < nflat; idx += blockDim.x) T.cstart[idx] = 0;
+  }
+#endif
   __syncthreads();
   S(d, 0);
   if (threadIdx.x < 64) {  // home segment lengths -> entries before each segment
     const int seg = threadIdx.x;
-    const int len = seg < nhseg ? T.hs[seg][home] - T.hs[seg][0] : 0;
+    const int len = seg < nhseg ? T.hs[seg][mw] - T.hs[seg][0] : 0;
     int inc = len;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -2395,28 +2455,43 @@ __device__ bool tile_load(const KParams& P, const Dev& d, int tx, int ty, TileLd
     }
     const int total = __shfl(inc, 63, 64);
     if (seg <= nhseg) T.hoff[seg] = inc - len;
-    if (seg == 0) T.nseq = 2 * total + (int)min(d.ctl->n_outl, d.outl_cap);
+    if (seg < nhseg) T.hbase[seg] = T.hs[seg][0] - (inc - len);
+    if (seg == 0) {
+      T.nhome = total;
+      T.nseq = 2 * total + (int)min(d.ctl->n_outl, d.outl_cap);
+    }
   }
+  __syncthreads();
+  if (T.nhome <= HTAG_MAX)  // home entry -> (segment, column) tags, one thread per home cell
+    for (int idx = threadIdx.x; idx < nhseg * mw; idx += blockDim.x) {
+      const int seg = idx / mw, hx = idx - seg * mw;
+      const int e0 = T.hoff[seg] + (T.hs[seg][hx] - T.hs[seg][0]), e1 = e0 + (T.hs[seg][hx + 1] - T.hs[seg][hx]);
+      for (int e = e0; e < e1; ++e) T.htag[e] = (uint16_t)(seg | hx << 8);
+    }
   __syncthreads();
   S(d, 1);
   const int nseq = T.nseq;
-  const bool one = nseq <= 4 * (int)blockDim.x;  // every element held in registers through the binning
-  Rec rr[4];
-  int cell[4], rank[4], gi[4];
-  // elements base + k·blockDim + tid (four in flight per thread): record,
-  // global index, flat cell index (-1: not in the block + halo)
+#ifndef STAGE_NE
+#define STAGE_NE 4
+#endif
+  constexpr int NE = STAGE_NE;  // elements per thread in flight
+  const bool one = nseq <= NE * (int)blockDim.x;  // every element held in registers through the binning
+  Rec rr[NE];
+  int cell[NE], rank[NE], gi[NE];
+  // elements base + k·blockDim + tid: record, global index, flat cell index
+  // (-1: not in the block + halo)
   auto fetch = [&](int base) {
-    int ax[4], ay[4], kd[4];
+    int ax[NE], ay[NE], kd[NE];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < NE; ++k) {
       const int q = base + k * (int)blockDim.x + (int)threadIdx.x;
-      gi[k] = q < nseq ? tile_elem(P, d, T, G, q, ax[k], ay[k], kd[k]) : -1;
+      gi[k] = q < nseq ? tile_elem(d, T, G, q, ax[k], ay[k], kd[k]) : -1;
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
+    for (int k = 0; k < NE; ++k)
       if (gi[k] >= 0) rr[k] = d.rec[gi[k]];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < NE; ++k) {
       cell[k] = -1;
       if (gi[k] < 0) continue;
       int x = ax[k], y = ay[k];
@@ -2427,21 +2502,21 @@ __device__ bool tile_load(const KParams& P, const Dev& d, int tx, int ty, TileLd
         y += c / 3 - 1;
       }
       const int hx = x - G.cx0, hy = y - G.cy0;
-      if (hx < 0 || hx >= halo || hy < 0 || hy >= halo) continue;
-      const int kind = (rr[k].id.x & RID_PID) >= P.NA;
-      cell[k] = (hy * 2 + kind) * (halo + 1) + hx;
+      if (hx < 0 || hx >= hw || hy < 0 || hy >= hh) continue;
+      const int kind = (rr[k].id.x & RID_LIG) ? 1 : 0, seg = hy * 2 + kind;
+      cell[k] = (seg * (hw + 1) + hx) | (seg | hx << 8) << 16;  // flat cell | LDS tag << 16
     }
   };
   auto count = [&]() {
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (cell[k] >= 0) rank[k] = atomicAdd(&T.cstart[cell[k]], 1);
+    for (int k = 0; k < NE; ++k)
+      if (cell[k] >= 0) rank[k] = atomicAdd(&T.cstart[cell[k] & 0xffff], 1);
   };
   if (one) {
     fetch(0);
     count();
   } else {
-    for (int base = 0; base < nseq; base += 4 * blockDim.x) {
+    for (int base = 0; base < nseq; base += NE * blockDim.x) {
       fetch(base);
       count();
     }
@@ -2452,26 +2527,25 @@ __device__ bool tile_load(const KParams& P, const Dev& d, int tx, int ty, TileLd
   if (threadIdx.x == 0) T.n = n;
   S(d, 3);
   if (n > P.tcap) return false;
-  auto place = [&](int k, int l, int g) {
+  // LDS record: the home position in place of the slot (tile_global)
+  auto place = [&](int k, int l) {
     T.pos[l] = rr[k].pos;
-    T.id[l] = rr[k].id;
-    T.gidx[l] = g;
+    T.id[l] = make_int2((gi[k] >> 1) | (rr[k].id.x & ~RID_PID), rr[k].id.y);
     if (site) site[l] = rr[k].site;
-    const int c = cell[k], seg = c / (halo + 1), hx = c - seg * (halo + 1);
-    T.tag[l] = (uint16_t)(seg | hx << 8);
+    T.tag[l] = (uint16_t)(cell[k] >> 16);
   };
   if (one) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (cell[k] >= 0) place(k, T.cstart[cell[k]] + rank[k], gi[k]);
+    for (int k = 0; k < NE; ++k)
+      if (cell[k] >= 0) place(k, T.cstart[cell[k] & 0xffff] + rank[k]);
   } else {
     // a second pass with the counters as cursors: each ends at its cell's
     // end (= the next cell's start), shifted back afterwards
-    for (int base = 0; base < nseq; base += 4 * blockDim.x) {
+    for (int base = 0; base < nseq; base += NE * blockDim.x) {
       fetch(base);
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (cell[k] >= 0) place(k, atomicAdd(&T.cstart[cell[k]], 1), gi[k]);
+      for (int k = 0; k < NE; ++k)
+        if (cell[k] >= 0) place(k, atomicAdd(&T.cstart[cell[k] & 0xffff], 1));
     }
     __syncthreads();
     int v[4];
@@ -2495,10 +2569,10 @@ __device__ bool tile_load(const KParams& P, const Dev& d, int tx, int ty, TileLd
 // Record ranges of the neighbour kind `kind` around the record at (seg, hx),
 // float position (px, py), cut to the cells within `reach` of it: three row
 // ranges (empty when the row is out of reach).
-__device__ __forceinline__ void item_ranges(const KParams& P, const TileLds& T, int tx, int ty, int seg, int hx,
+__device__ __forceinline__ void item_ranges(const KParams& P, const TileLds& T, const TileGeo& G, int seg, int hx,
                                            float px, float py, int kind, float reach, int* r0, int* r1) {
   const int hy = seg >> 1;
-  const int cx = tx * P.tile - 1 + hx, cy = ty * P.tile - 1 + hy;
+  const int cx = G.cx0 + hx, cy = G.cy0 + hy;
   const float xb = (float)(P.gx0 + cx * P.cs), yb = (float)(P.gy0 + cy * P.cs), cs = (float)P.cs;
   const int lo = hx - (px - xb < reach ? 1 : 0), hi = hx + (xb + cs - px < reach ? 1 : 0);
   const bool down = py - yb < reach, up = yb + cs - py < reach;
@@ -2506,8 +2580,8 @@ __device__ __forceinline__ void item_ranges(const KParams& P, const TileLds& T, 
   for (int k = 0; k < 3; ++k) {
     const int s = (hy - 1 + k) * 2 + kind;
     const bool on = k == 1 || (k == 0 ? down : up);
-    r0[k] = on ? tcs(T, P.tile + 2, s, lo) : 0;
-    r1[k] = on ? tcs(T, P.tile + 2, s, hi + 1) : 0;
+    r0[k] = on ? tcs(T, G.hw, s, lo) : 0;
+    r1[k] = on ? tcs(T, G.hw, s, hi + 1) : 0;
   }
 }
 
@@ -2521,15 +2595,15 @@ __device__ __forceinline__ void item_ranges(const KParams& P, const TileLds& T, 
 // neighbour records of consecutive lanes are mostly consecutive.
 // chk(l, r) for every pair; all threads call (no barrier).
 template <class Rng, class Chk>
-__device__ __forceinline__ void tile_walk(const KParams& P, const TileLds& T, Rng rng, Chk chk) {
-  const int tile = P.tile, n = T.n, lane = __lane_id();
+__device__ __forceinline__ void tile_walk(const TileGeo& G, const TileLds& T, Rng rng, Chk chk) {
+  const int n = T.n, lane = __lane_id();
   for (int base = 0; base < n; base += blockDim.x) {
     const int l = base + threadIdx.x;
     int r0[6], r1[6];
     bool item = false;
     if (l < n) {
       const int tg = T.tag[l], seg = tg & 0xff, hx = tg >> 8, hy = seg >> 1;
-      if (hy >= 1 && hy <= tile && hx >= 1 && hx <= tile) item = rng(l, seg, hx, r0, r1);
+      if (hy >= 1 && hy <= G.h && hx >= 1 && hx <= G.w) item = rng(l, seg, hx, r0, r1);
     }
     // range starts | pairs before the range << 16 (LDS indices < TCAP, counts < 6 TCAP)
     uint32_t pk[6];
@@ -2569,15 +2643,17 @@ __device__ __forceinline__ void tile_walk(const KParams& P, const TileLds& T, Rn
 
 // Up to four (a, b) entries held in registers per lane while pairs are
 // checked; the lanes of a wave then reserve their slots with one LDS atomic.
+// (LDS indices packed a | b << 16: TCAP < 2^16)
 struct PairBuf {
-  int2 v0, v1, v2, v3;
+  uint32_t v0, v1, v2, v3;
   int n;
 };
 __device__ __forceinline__ void pair_push(PairBuf& b, int2 v) {
-  b.v0 = b.n == 0 ? v : b.v0;
-  b.v1 = b.n == 1 ? v : b.v1;
-  b.v2 = b.n == 2 ? v : b.v2;
-  b.v3 = b.n == 3 ? v : b.v3;
+  const uint32_t x = (uint32_t)v.x | (uint32_t)v.y << 16;
+  b.v0 = b.n == 0 ? x : b.v0;
+  b.v1 = b.n == 1 ? x : b.v1;
+  b.v2 = b.n == 2 ? x : b.v2;
+  b.v3 = b.n == 3 ? x : b.v3;
   ++b.n;
 }
 // active lanes of a wave; entries mapped through f on the way out
@@ -2594,7 +2670,8 @@ __device__ __forceinline__ void pair_flush(const PairBuf& b, WgList& L, const SL
   if (__lane_id() == leader) base = atomicAdd(&L.n, tot);
   base = __shfl(base, leader, 64);
   for (int k = 0; k < n; ++k) {
-    const int2 v = f(k == 0 ? b.v0 : k == 1 ? b.v1 : k == 2 ? b.v2 : b.v3);
+    const uint32_t x = k == 0 ? b.v0 : k == 1 ? b.v1 : k == 2 ? b.v2 : b.v3;
+    const int2 v = f(make_int2((int)(x & 0xffffu), (int)(x >> 16)));
     const uint32_t s = base + pre + k;
     if (s < EBUF) {
       L.buf[s] = v;
@@ -2630,12 +2707,33 @@ __device__ __forceinline__ void col_emit(const Dev& d, WgList& L, int rs, int rg
 }
 
 // the fate-independent filters + prefilter for one (proposal, record) pair
-__device__ __forceinline__ bool col_pair(int NA, int2 me, float4 mp, int2 id, float4 rp) {
+// (records identified by slot or by home position: both unique per protein)
+__device__ __forceinline__ bool col_pair(int2 me, float4 mp, int2 id, float4 rp) {
   const int m = me.x & RID_PID, u = me.y;
   const int q = id.x & RID_PID, kq = id.y;
   const bool isnew = id.x < 0;
   const bool own_ok = kq == u ? isnew : (kq > u ? !isnew : true);
-  return (q != m) & own_ok & prefilter(m < NA, mp.x, mp.y, mp.z, mp.w, q < NA, rp);
+  return (q != m) & own_ok & prefilter(!(me.x & RID_LIG), mp.x, mp.y, mp.z, mp.w, !(id.x & RID_LIG), rp);
+}
+
+// the receptor of record `me` can take part in a reaction (either bond free)
+__device__ __forceinline__ bool rxn_item(int2 me) {
+  return !(me.x & RID_LIG) && !((me.x & RID_ST2) && (me.x & RID_ST3));
+}
+
+// prefilter of one (receptor record, record) pair, finality aside
+__device__ __forceinline__ bool rxn_pair(int2 me, float4 mp, float2 ms, int2 id, float4 rp, float2 qs) {
+  const int i = me.x & RID_PID, q = id.x & RID_PID;
+  const bool isB = (id.x & RID_LIG) != 0;
+  const float dx = rp.x - mp.x, dy = rp.y - mp.y;
+  const float dxy2 = dx * dx + dy * dy;
+  const bool rl_ok = isB & !(me.x & RID_ST2) & (dxy2 < 105.0f * 105.0f) & (rp.z > mp.z - 85.0f) &
+                     (rp.z < mp.w + 85.0f);
+  const float gap = fmaxf(fmaxf(rp.z - mp.w, mp.z - rp.w), 0.0f);
+  const float tx = qs.x - ms.x, ty = qs.y - ms.y;
+  const bool cis_ok = !isB & !(me.x & RID_ST3) & !(id.x & RID_ST3) & (dxy2 < 57.0f * 57.0f) & (gap < 16.0f) &
+                      (tx * tx + ty * ty < 16.0f * 16.0f);
+  return (q != i) & (rl_ok | cis_ok);
 }
 
 // ---------------------------------------------------------------- 4b. exact
@@ -2650,29 +2748,106 @@ __device__ __forceinline__ void mark_rej(const Dev& d, int u, uint32_t tag) {
 // (own unit, or a later unit's old position) rejects u outright; one with an
 // earlier unit's record becomes a conflict entry (u, kq, isnew) for pass C.
 // Unit states this step: untouched = accepted, S_PEND, S_REJ (atomicMax).
+// one candidate (proposal record a, record b)
+__device__ __forceinline__ void col_exact_one(const KParams& P, const Dev& d, int2 a, int2 b, uint32_t tag) {
+  int m = a.x & RID_PID, u = a.y, q = b.x & RID_PID, kq = b.y;
+  bool isnew = b.x < 0;
+  Own o;
+  load_own(P, d.nxt, m, o);
+  if (!exact_collide(P, o, isnew ? d.nxt : d.cur, q)) return;
+  if (kq >= u) {
+    mark_rej(d, u, tag);
+    return;
+  }
+  uint32_t old = atomicMax(&d.ustate[u], tag | S_PEND);
+  if ((old & ~3u) != tag) {
+    sl_push(d.plist, make_int2(u, 0), &d.ctl->err);  // at most one entry per unit
+  } else if ((old & 3u) == S_REJ) {
+    return;
+  }
+  sl_push(d.conf, make_int2(u, kq | (isnew ? (int)0x80000000 : 0)), &d.ctl->err);
+}
+
+// Records of a dense block's staging sequence (the home records of its home
+// region, then the outlier list) from global memory: f(record index) for
+// elements start, start + stride, ...  A home record coded RID_OUT is
+// skipped (it is on the outlier list).
+template <class F>
+__device__ __forceinline__ void dense_records(const KParams& P, const Dev& d, const TileGeo& G, int start, int stride,
+                                              F f) {
+  const int xlo = max(G.hx0, 0), xhi = min(G.hx0 + G.mw - 1, P.ncx - 1);
+  int q = 0;  // running element index
+  for (int seg = 0; seg < G.nhseg; ++seg) {
+    const int y = G.hy0 + (seg >> 1);
+    if (y < 0 || y >= P.ncy || xlo > xhi) continue;
+    const int lo = d.hstart[cell_index(P, xlo, y, seg & 1)], hi = d.hstart[cell_index(P, xhi + 1, y, seg & 1)];
+    const int n = 2 * (hi - lo);
+    for (int k = ((start - q) % stride + stride) % stride; k < n; k += stride) {
+      const int ri = 2 * lo + k;
+      if (rec_code(d.rec[ri].id) != RID_OUT) f(ri);
+    }
+    q += n;
+  }
+  const int no = (int)min(d.ctl->n_outl, d.outl_cap);
+  for (int k = ((start - q) % stride + stride) % stride; k < no; k += stride) f(d.outl[k].x);
+}
+
+// the exact cell of record ri (from its beads: R for the old position, R_new
+// for the proposal)
+__device__ __forceinline__ void rec_cell_exact(const KParams& P, const Dev& d, int ri, int& cx, int& cy) {
+  const int2 id = d.rec[ri].id;
+  const int p = id.x & RID_PID;
+  const Beads& B = id.x < 0 ? d.nxt : d.cur;
+  cx = cell_x(P, B.P(p, 1, 1, 0));
+  cy = cell_y(P, B.P(p, 1, 1, 1));
+}
+
+// Brute force over a dense block (k_pair_scan could not stage it): every
+// record of the block against every record of the 3x3 cells around it —
+// collision candidates tested here at once, reaction candidates emitted.
+#ifdef DENSE_NOINLINE  // (A/B builds)
+__device__ __noinline__
+#else
+__device__ __forceinline__
+#endif
+void dense_block(const KParams& P, const Dev& d, int4 blk, uint32_t tag) {
+  const TileGeo G = tile_geo(blk.x, blk.y, blk.z, blk.w);
+  dense_records(P, d, G, threadIdx.x, blockDim.x, [&](int ri) {
+    int x, y;
+    rec_cell_exact(P, d, ri, x, y);
+    if (x < G.x0 || x >= G.x0 + G.w || y < G.y0 || y >= G.y0 + G.h) return;
+    const Rec mr = d.rec[ri];
+    const int2 me = mr.id;
+    bool prop = me.x < 0;
+    if (prop && me.y < 0) {
+      atomicOr(&d.ctl->err, ERR_RESOLVE);
+      prop = false;
+    }
+    const bool rx = rxn_item(me);
+    if (!prop && !rx) return;
+    dense_records(P, d, G, 0, 1, [&](int rn) {
+      int ox, oy;
+      rec_cell_exact(P, d, rn, ox, oy);
+      if (abs(ox - x) > 1 || abs(oy - y) > 1) return;
+      const Rec o = d.rec[rn];
+      if (prop && col_pair(me, mr.pos, o.id, o.pos)) {
+        if (o.id.y < 0) atomicOr(&d.ctl->err, ERR_RESOLVE);
+        else col_exact_one(P, d, me, o.id, tag);
+      }
+      if (rx && rxn_pair(me, mr.pos, mr.site, o.id, o.pos, o.site)) sl_push(d.pairs, make_int2(ri, rn), &d.ctl->err);
+    });
+  });
+}
+
 __global__ void k_col_exact(KParams P, Dev d) {
   const uint32_t tag = (d.ctl->step & 0x3fffffffu) << 2;
   __shared__ uint32_t pre[NSHARD + 1];
+  const uint32_t nd = min(d.ctl->n_dense, d.dense_cap);
+  for (uint32_t b = blockIdx.x; b < nd; b += gridDim.x) dense_block(P, d, d.dense[b], tag);
   const uint32_t n = sl_prefix(d.cand, pre);
   for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
-    int2 c = sl_at(d.cand, pre, t);
-    int2 a = d.rec[c.x].id, b = d.rec[c.y].id;
-    int m = a.x & RID_PID, u = a.y, q = b.x & RID_PID, kq = b.y;
-    bool isnew = b.x < 0;
-    Own o;
-    load_own(P, d.nxt, m, o);
-    if (!exact_collide(P, o, isnew ? d.nxt : d.cur, q)) continue;
-    if (kq >= u) {
-      mark_rej(d, u, tag);
-      continue;
-    }
-    uint32_t old = atomicMax(&d.ustate[u], tag | S_PEND);
-    if ((old & ~3u) != tag) {
-      sl_push(d.plist, make_int2(u, 0), &d.ctl->err);  // at most one entry per unit
-    } else if ((old & 3u) == S_REJ) {
-      continue;
-    }
-    sl_push(d.conf, make_int2(u, kq | (isnew ? (int)0x80000000 : 0)), &d.ctl->err);
+    const int2 c = sl_at(d.cand, pre, t);
+    col_exact_one(P, d, d.rec[c.x].id, d.rec[c.y].id, tag);
   }
 }
 
@@ -2823,141 +2998,96 @@ __device__ __forceinline__ void rxn_emit(const Dev& d, WgList& L, int a, int b) 
   wg_emit(L, make_int2(a, b), d.pairs, &d.ctl->err);
 }
 
-// the receptor of record `me` can take part in a reaction (either bond free)
-__device__ __forceinline__ bool rxn_item(int NA, int2 me) {
-  return (me.x & RID_PID) < NA && !((me.x & RID_ST2) && (me.x & RID_ST3));
-}
-
-// prefilter of one (receptor record, record) pair, finality aside
-__device__ __forceinline__ bool rxn_pair(int NA, int2 me, float4 mp, float2 ms, int2 id, float4 rp, float2 qs) {
-  const int i = me.x & RID_PID, q = id.x & RID_PID;
-  const bool isB = q >= NA;
-  const float dx = rp.x - mp.x, dy = rp.y - mp.y;
-  const float dxy2 = dx * dx + dy * dy;
-  const bool rl_ok = isB & !(me.x & RID_ST2) & (dxy2 < 105.0f * 105.0f) & (rp.z > mp.z - 85.0f) &
-                     (rp.z < mp.w + 85.0f);
-  const float gap = fmaxf(fmaxf(rp.z - mp.w, mp.z - rp.w), 0.0f);
-  const float tx = qs.x - ms.x, ty = qs.y - ms.y;
-  const bool cis_ok = !isB & !(me.x & RID_ST3) & !(id.x & RID_ST3) & (dxy2 < 57.0f * 57.0f) & (gap < 16.0f) &
-                      (tx * tx + ty * ty < 16.0f * 16.0f);
-  return (q != i) & (rl_ok | cis_ok);
-}
-
 // ---------------------------------------------------------------- pair scan
 // One staging of each tile for both pair searches of the step: collision
 // candidates of the proposal records (pass A, §4a) and reaction candidates of
 // the records of receptors that can react (above).  An item's stencil is cut
 // to the larger of its two reaches per neighbour kind; each pair is tested
 // against both filters.
-__global__ void __launch_bounds__(256) k_pair_scan(KParams P, Dev d) {
+// Stage block G and walk its pairs (false: more than tcap records, nothing
+// emitted; the block then goes onto the dense list, k_col_exact).
+__device__ __forceinline__ bool pair_scan_block(const KParams& P, const Dev& d, const TileGeo& G, TileLds& T,
+                                                float2* site, WgList& Lc, WgList& Lr, Stamper& S) {
+  const int NB = P.NB;
+  if (!tile_load(P, d, G, T, site, S)) return false;
+  if (P.dbg_stage == 1) return true;
+  PairBuf Bc, Br;
+  Bc.n = 0;
+  Br.n = 0;
+  tile_walk(
+      G, T,
+      [&](int l, int seg, int hx, int* r0, int* r1) {
+        const int2 me = T.id[l];
+        bool prop = me.x < 0;  // proposal record: collision candidates
+        if (prop && me.y < 0) {
+          atomicOr(&d.ctl->err, ERR_RESOLVE);
+          prop = false;
+        }
+        const bool rx = rxn_item(me);
+        if (!prop && !rx) return false;
+        const bool mA = !(me.x & RID_LIG);
+        float reach0 = prop ? (mA ? REACH_AA : REACH_AB) : 0.0f;
+        float reach1 = prop ? (mA ? REACH_AB : REACH_BB) : 0.0f;
+        if (rx && !(me.x & RID_ST3)) reach0 = fmaxf(reach0, REACH_CIS);
+        if (rx && !(me.x & RID_ST2) && NB > 0) reach1 = fmaxf(reach1, REACH_RL);
+        const float4 mp = T.pos[l];
+        item_ranges(P, T, G, seg, hx, mp.x, mp.y, 0, reach0, r0, r1);
+        item_ranges(P, T, G, seg, hx, mp.x, mp.y, 1, reach1, r0 + 3, r1 + 3);
+        if (reach0 == 0.0f)
+          for (int k = 0; k < 3; ++k) r1[k] = r0[k];
+        if (reach1 == 0.0f)
+          for (int k = 3; k < 6; ++k) r1[k] = r0[k];
+        return true;
+      },
+      [&](int il, int nl) {
+        const int2 me = T.id[il], id = T.id[nl];
+        const float4 mp = T.pos[il], rp = T.pos[nl];
+        if (me.x < 0 && me.y >= 0 && col_pair(me, mp, id, rp)) {
+          if (id.y < 0) atomicOr(&d.ctl->err, ERR_RESOLVE);
+          else if (Bc.n < 4) pair_push(Bc, make_int2(il, nl));
+          else col_emit(d, Lc, tile_global(T, il), tile_global(T, nl));
+        }
+        if (rxn_item(me) && rxn_pair(me, mp, site[il], id, rp, site[nl])) {
+          if (Br.n < 4) pair_push(Br, make_int2(il, nl));
+          else rxn_emit(d, Lr, tile_global(T, il), tile_global(T, nl));
+        }
+      });
+  S(d, 5);
+  auto glb = [&](int2 v) { return make_int2(tile_global(T, v.x), tile_global(T, v.y)); };
+  pair_flush(Bc, Lc, d.cand, &d.ctl->err, glb);
+  pair_flush(Br, Lr, d.pairs, &d.ctl->err, glb);
+  S(d, 6);
+  return true;
+}
+
+// One workgroup per tile.  A tile whose records overflow TCAP (never at the
+// benchmark densities with the host's tile choice) goes onto the dense list,
+// which k_col_exact scans by brute force from global memory: this kernel
+// stays free of that path's registers and call frame (measured: a fallback
+// inside costs it a third of its speed, through the lost occupancy or the
+// scratch frame).
+#ifndef PAIR_WAVES  // minimum waves per SIMD of the pair scan (A/B builds: tools/build_variants.py)
+#define PAIR_WAVES 5
+#endif
+__global__ void __launch_bounds__(256, PAIR_WAVES) k_pair_scan(KParams P, Dev d) {
   __shared__ TileLds T;
   __shared__ float2 site[TCAP];
   __shared__ WgList Lc, Lr;
-  const int NA = P.NA, NB = P.NB;
   const int ntx = (P.ncx + P.tile - 1) / P.tile;
   const int tx = blockIdx.x % ntx, ty = blockIdx.x / ntx;
+  const int x0 = tx * P.tile, y0 = ty * P.tile, w = min(P.tile, P.ncx - x0), h = min(P.tile, P.ncy - y0);
   wg_list_init(Lc);
   wg_list_init(Lr);
   Stamper S(0);
-  TileGeo G;
-  if (tile_load(P, d, tx, ty, T, site, S, G)) {
-    if (P.dbg_stage == 1) return;
-    PairBuf Bc, Br;
-    Bc.n = 0;
-    Br.n = 0;
-    tile_walk(
-        P, T,
-        [&](int l, int seg, int hx, int* r0, int* r1) {
-          const int2 me = T.id[l];
-          bool prop = me.x < 0;  // proposal record: collision candidates
-          if (prop && me.y < 0) {
-            atomicOr(&d.ctl->err, ERR_RESOLVE);
-            prop = false;
-          }
-          const bool rx = rxn_item(NA, me);
-          if (!prop && !rx) return false;
-          const bool mA = (me.x & RID_PID) < NA;
-          float reach0 = prop ? (mA ? REACH_AA : REACH_AB) : 0.0f;
-          float reach1 = prop ? (mA ? REACH_AB : REACH_BB) : 0.0f;
-          if (rx && !(me.x & RID_ST3)) reach0 = fmaxf(reach0, REACH_CIS);
-          if (rx && !(me.x & RID_ST2) && NB > 0) reach1 = fmaxf(reach1, REACH_RL);
-          const float4 mp = T.pos[l];
-          item_ranges(P, T, tx, ty, seg, hx, mp.x, mp.y, 0, reach0, r0, r1);
-          item_ranges(P, T, tx, ty, seg, hx, mp.x, mp.y, 1, reach1, r0 + 3, r1 + 3);
-          if (reach0 == 0.0f)
-            for (int k = 0; k < 3; ++k) r1[k] = r0[k];
-          if (reach1 == 0.0f)
-            for (int k = 3; k < 6; ++k) r1[k] = r0[k];
-          return true;
-        },
-        [&](int il, int nl) {
-          const int2 me = T.id[il], id = T.id[nl];
-          const float4 mp = T.pos[il], rp = T.pos[nl];
-          if (me.x < 0 && me.y >= 0 && col_pair(NA, me, mp, id, rp)) {
-            if (id.y < 0) atomicOr(&d.ctl->err, ERR_RESOLVE);
-            else if (Bc.n < 4) pair_push(Bc, make_int2(il, nl));
-            else col_emit(d, Lc, tile_global(T, il), tile_global(T, nl));
-          }
-          if (rxn_item(NA, me) && rxn_pair(NA, me, mp, site[il], id, rp, site[nl])) {
-            if (Br.n < 4) pair_push(Br, make_int2(il, nl));
-            else rxn_emit(d, Lr, tile_global(T, il), tile_global(T, nl));
-          }
-        });
-    S(d, 5);
-    auto glb = [&](int2 v) { return make_int2(tile_global(T, v.x), tile_global(T, v.y)); };
-    pair_flush(Bc, Lc, d.cand, &d.ctl->err, glb);
-    pair_flush(Br, Lr, d.pairs, &d.ctl->err, glb);
-    S(d, 6);
-    if (P.dbg_stage == 3) return;
-    wg_flush(Lc, d.cand, &d.ctl->err);
-    wg_flush(Lr, d.pairs, &d.ctl->err);
-    S(d, 7);
-    return;
+  if (!pair_scan_block(P, d, tile_geo(x0, y0, w, h), T, site, Lc, Lr, S) && threadIdx.x == 0) {
+    const uint32_t o = atomicAdd(&d.ctl->n_dense, 1u);  // k_col_exact takes it
+    if (o < d.dense_cap) d.dense[o] = make_int4(x0, y0, w, h);
+    else atomicOr(&d.ctl->err, ERR_EDGES);
   }
-  // dense tile (more than tcap records): every interior record of the
-  // staging sequence against every sequence record of its 3x3 cells, records
-  // from global memory (never at the benchmark densities; KMC_DEBUG_TCAP)
-  const int nseq = T.nseq;
-  auto elem = [&](int q, Rec& r, int& x, int& y) -> int {
-    int kd;
-    const int ri = tile_elem(P, d, T, G, q, x, y, kd);
-    if (ri < 0) return -1;
-    r = d.rec[ri];
-    if (kd >= 0) {
-      const int c = rec_code(r.id);
-      if (c == RID_OUT) return -1;
-      x += c % 3 - 1;
-      y += c / 3 - 1;
-    }
-    return ri;
-  };
-  for (int qi = threadIdx.x; qi < nseq; qi += blockDim.x) {
-    Rec mr;
-    int x, y;
-    const int ri = elem(qi, mr, x, y);
-    if (ri < 0 || x - G.cx0 < 1 || x - G.cx0 > P.tile || y - G.cy0 < 1 || y - G.cy0 > P.tile) continue;
-    const int2 me = mr.id;
-    bool prop = me.x < 0;
-    if (prop && me.y < 0) {
-      atomicOr(&d.ctl->err, ERR_RESOLVE);
-      prop = false;
-    }
-    const bool rx = rxn_item(NA, me);
-    if (!prop && !rx) continue;
-    for (int qn = 0; qn < nseq; ++qn) {
-      Rec o;
-      int ox, oy;
-      const int rn = elem(qn, o, ox, oy);
-      if (rn < 0 || abs(ox - x) > 1 || abs(oy - y) > 1) continue;
-      if (prop && col_pair(NA, me, mr.pos, o.id, o.pos)) {
-        if (o.id.y < 0) atomicOr(&d.ctl->err, ERR_RESOLVE);
-        else col_emit(d, Lc, ri, rn);
-      }
-      if (rx && rxn_pair(NA, me, mr.pos, mr.site, o.id, o.pos, o.site)) rxn_emit(d, Lr, ri, rn);
-    }
-  }
+  if (P.dbg_stage == 1 || P.dbg_stage == 3) return;
   wg_flush(Lc, d.cand, &d.ctl->err);
   wg_flush(Lr, d.pairs, &d.ctl->err);
+  S(d, 7);
 }
 
 // Reaction candidates, pass 2: exact R–L association gates (main.cpp:1880-1921)
@@ -3427,6 +3557,7 @@ __global__ void __launch_bounds__(256) k_finalize(KParams P, Dev d, double time_
   c->n_rl = 0;
   c->n_cisc = 0;
   c->n_outl = 0;
+  c->n_dense = 0;
 }
 
 
