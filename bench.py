@@ -197,6 +197,11 @@ def main(argv=None):
 
 
 def run_rank(args, rank: int, world: int, local: int):
+    # stdout carries exactly one JSON line: native libraries (RCCL prints its
+    # version banner to stdout at communicator init) write to stderr instead
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     import torch
     import torch.distributed as dist
 
@@ -373,7 +378,7 @@ def run_rank(args, rank: int, world: int, local: int):
             "ensemble_reduce": reduce_info,
             "library": library,
         }
-        print(json.dumps(line), flush=True)
+        os.write(json_fd, (json.dumps(line) + "\n").encode())
     sim.close()
     dist.destroy_process_group()
 
