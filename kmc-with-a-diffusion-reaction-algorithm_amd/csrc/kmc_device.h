@@ -31,6 +31,7 @@ struct KParams {
   int tcap;  // LDS tile record capacity (<= TCAP; lowered only to test the global path)
   int tile;  // cells per tile side of the LDS scans (<= TILE_MAX)
   int dbg_stage;  // debug timing only: stop the tile scans after stage 1 (load) / 2 (items); 0 = off
+  int tout_cap;   // per-tile outlier bucket capacity (<= TOUT_CAP; lowered only by KMC_DEBUG_TOUT_CAP)
   int cx_serial;  // debug: complexes aligned by one lane (KMC_CX_SERIAL=1) instead of the whole wave
   uint32_t cx_limit;  // members[] cursor above which k_finalize latches a full complex rebuild (mcap / 2;
                       // lowered only by KMC_DEBUG_CX_LIMIT to exercise the rebuild)
@@ -63,7 +64,7 @@ struct Ctl {
   uint32_t force_full;    // k_finalize: the next step's k_cx_kill rebuilds every complex (members[] half
                           // full, or a dirty list overflowed); only k_finalize writes it
   uint32_t n_forced;      // diagnostics: full complex rebuilds latched by force_full since the state was set
-  uint32_t pad3;
+  uint32_t last_outl;     // diagnostics: the previous step's outlier records (n_outl)
   uint64_t vtag;          // BFS tag counter for the overflow path
   uint64_t stamps[24];    // diagnostic build (-DKMC_STAMPS) only: phase cycles (tile scans, complexes)
 };

@@ -39,6 +39,7 @@ struct kmc_sim {
   int64_t step_done = 0;
   std::string err;
   int ncell = 0;
+  int ntiles = 0;  // pair-scan tiles (K.tile × K.tile cells each)
   bool have_state = false;
   std::vector<void*> allocs;
   kmc_obs_dev* obs_buf = nullptr;
@@ -366,6 +367,10 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   const char* tc = getenv("KMC_DEBUG_TCAP");
   K.tcap = TCAP;
   if (tc && *tc) K.tcap = std::max(0, std::min(TCAP, atoi(tc)));
+  // debug: smaller per-tile outlier buckets, so that tiles fall back to the whole outlier list
+  const char* oc = getenv("KMC_DEBUG_TOUT_CAP");
+  K.tout_cap = TOUT_CAP;
+  if (oc && *oc) K.tout_cap = std::max(0, std::min(TOUT_CAP, atoi(oc)));
   // tile side of the LDS scans: about 200 proposal records per 256-thread
   // workgroup, halo records well inside TCAP (mean density of the box)
   {
@@ -414,6 +419,14 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
     }
     s->scan_tmp_bytes = std::max<size_t>(tb, 16);
     if (dalloc(s, (uint8_t**)&s->scan_tmp, s->scan_tmp_bytes) != KMC_OK) {
+      kmc_destroy(s);
+      return KMC_ERR_HIP;
+    }
+    // per-tile outlier buckets of the pair scan (counters zero between steps)
+    s->ntiles = ((K.ncx + K.tile - 1) / K.tile) * ((K.ncy + K.tile - 1) / K.tile);
+    if (dalloc(s, &s->d.tout, (size_t)s->ntiles * TOUT_CAP) != KMC_OK ||
+        dalloc(s, &s->d.tout_n, (size_t)s->ntiles) != KMC_OK ||
+        hipMemset(s->d.tout_n, 0, sizeof(uint32_t) * (size_t)s->ntiles) != hipSuccess) {
       kmc_destroy(s);
       return KMC_ERR_HIP;
     }
@@ -525,6 +538,7 @@ static int clear_step_tags(kmc_sim* s) {
   // chunk's tags would match the replayed steps' numbers
   HIPCHK(s, hipMemsetAsync(d.bfs_cand, 0, sizeof(uint32_t) * (size_t)s->K.NB, st));
   HIPCHK(s, hipMemsetAsync(d.shuf_tag, 0, sizeof(uint32_t) * (size_t)s->K.NB, st));
+  HIPCHK(s, hipMemsetAsync(d.tout_n, 0, sizeof(uint32_t) * (size_t)s->ntiles, st));
   return KMC_OK;
 }
 
@@ -787,7 +801,7 @@ static int launch_step(kmc_sim* s, bool re_sort) {
     }
   }
   const int gX = std::min(2048, (K.N + T - 1) / T);  // grid-stride kernels over device-sized lists
-  const int ntiles = ((K.ncx + K.tile - 1) / K.tile) * ((K.ncy + K.tile - 1) / K.tile);
+  const int ntiles = s->ntiles;
   // collision candidates and reaction candidates, one staging of each tile
   TIMED(KI_PAIR_SCAN, (k_pair_scan<<<ntiles, 256, 0, st>>>(K, d)));
   // (at least 64 workgroups: k_col_exact also scans the dense blocks, one per workgroup)
@@ -946,8 +960,8 @@ int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out) {
     s->clusters_valid = true;
     if (s->debug_counts) {
       const uint32_t* l = s->ctl_host->last;
-      fprintf(stderr, "kmc step %lld: candidates %u conflicts %u pending-units %u rejected %u rxn-pairs %u rl-edges %u cis-edges %u bfs-overflow %u (list growth 2^%d, replays %lld, forced rebuilds %u)\n",
-              (long long)s->step_done, l[0], l[1], l[2], l[3], l[4], l[5], l[6], l[7], s->grow,
+      fprintf(stderr, "kmc step %lld: candidates %u conflicts %u pending-units %u rejected %u rxn-pairs %u rl-edges %u cis-edges %u bfs-overflow %u outliers %u (list growth 2^%d, replays %lld, forced rebuilds %u)\n",
+              (long long)s->step_done, l[0], l[1], l[2], l[3], l[4], l[5], l[6], l[7], s->ctl_host->last_outl, s->grow,
               (long long)s->n_replays, s->ctl_host->n_forced);
       const uint64_t* t = s->ctl_host->stamps;
       if (t[16])

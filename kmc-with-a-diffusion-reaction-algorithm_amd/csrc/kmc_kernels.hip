@@ -79,6 +79,9 @@ struct Dev {
   struct Rec* rec;      // [2N] records, home order; written by the kernels that move the protein
   int4* outl;           // [outl_cap] records more than one cell from their home cell: {record, cx, cy, -}
   uint32_t outl_cap;
+  int2* tout;           // [ntiles][TOUT_CAP] the outliers whose cell lies in a pair-scan tile's block + halo:
+                        //   {record, cx | cy << 16}
+  uint32_t* tout_n;     // [ntiles] entries of each tile's bucket this step (zeroed by the tile's k_pair_scan)
   int4* dense;          // [dense_cap] blocks of cells whose records overflow the pair scan's LDS: {x0, y0, w, h}
   uint32_t dense_cap;
   SList cand;           // collision candidates (proposal record, other record)
@@ -557,8 +560,28 @@ __device__ __forceinline__ int cell_index(const KParams& P, int cx, int cy, int 
 // re-sorts a record stays within one cell of its home cell: the record keeps
 // that offset (4-bit cell code), and a tile of the pair scan finds every
 // record of its cells (+ one-cell halo) among the home cells of the tile +
-// two cells.  A record further away (rare: re-sorts every 100 steps) goes
-// onto the outlier list that every tile also reads.
+// two cells.  A record further away goes onto the outlier list and into the
+// bucket of every tile whose block + one-cell halo holds its cell (up to
+// four).  Outliers are few but not rare: every protein that crossed the
+// periodic boundary since the last re-sort is one (thousands at C5 after 100
+// steps), so a tile reads only its own bucket — the whole list only when its
+// bucket overflowed.
+#ifndef TOUT_CAP
+#define TOUT_CAP 64
+#endif
+__device__ __forceinline__ void tile_bucket_push(const KParams& P, const Dev& d, int ri, int cx, int cy) {
+  const int t = P.tile, ntx = (P.ncx + t - 1) / t;
+  const int tx = cx / t, ty = cy / t, rx = cx - tx * t, ry = cy - ty * t;
+  const int x0 = tx - (rx == 0 && tx > 0 ? 1 : 0), x1 = tx + (rx == t - 1 && (tx + 1) * t < P.ncx ? 1 : 0);
+  const int y0 = ty - (ry == 0 && ty > 0 ? 1 : 0), y1 = ty + (ry == t - 1 && (ty + 1) * t < P.ncy ? 1 : 0);
+  for (int y = y0; y <= y1; ++y)
+    for (int x = x0; x <= x1; ++x) {
+      const int b = y * ntx + x;
+      const uint32_t o = atomicAdd(&d.tout_n[b], 1u);
+      if (o < (uint32_t)P.tout_cap) d.tout[(size_t)b * TOUT_CAP + o] = make_int2(ri, cx | cy << 16);
+    }
+}
+
 __device__ __forceinline__ void put_rec(const KParams& P, const Dev& d, uint2 h, int p, int w, int st, int own,
                                         double x, double y, double zlo, double zhi, double sx, double sy) {
   const int cx = cell_x(P, x), cy = cell_y(P, y);
@@ -571,6 +594,7 @@ __device__ __forceinline__ void put_rec(const KParams& P, const Dev& d, uint2 h,
     const uint32_t o = atomicAdd(&d.ctl->n_outl, 1u);
     if (o < d.outl_cap) d.outl[o] = make_int4(ri, cx, cy, 0);
     else atomicOr(&d.ctl->err, ERR_EDGES);
+    tile_bucket_push(P, d, ri, cx, cy);
   }
   Rec r;
   r.pos = make_float4((float)x, (float)y, (float)zlo, (float)zhi);
@@ -2317,6 +2341,8 @@ struct TileLds {
   int hoff[HSEG_MAX + 1];          // home entries before each home segment; [nhseg] = all
   uint16_t htag[HTAG_MAX];         // home segment | column << 8 of each home entry
   int n, nseq, nhome;
+  int obkt;                        // the block's outlier bucket (tile index), or -1: the whole outlier list
+  uint32_t nout;                   // entries of that bucket
 };
 __device__ __forceinline__ int tcs(const TileLds& T, int hw, int seg, int hx) { return T.cstart[seg * (hw + 1) + hx]; }
 
@@ -2390,6 +2416,13 @@ __device__ __forceinline__ int tile_elem(const Dev& d, const TileLds& T, const T
     kind = seg & 1;
     return 2 * (T.hbase[seg] + e) + w;
   }
+  if (T.obkt >= 0) {
+    const int2 o = d.tout[(size_t)T.obkt * TOUT_CAP + (q - 2 * nhome)];
+    ax = o.y & 0xffff;
+    ay = (int)((uint32_t)o.y >> 16);
+    kind = -1;
+    return o.x;
+  }
   const int4 o = d.outl[q - 2 * nhome];
   ax = o.y;
   ay = o.z;
@@ -2458,7 +2491,7 @@ __device__ bool tile_load(const KParams& P, const Dev& d, const TileGeo& G, Tile
     if (seg < nhseg) T.hbase[seg] = T.hs[seg][0] - (inc - len);
     if (seg == 0) {
       T.nhome = total;
-      T.nseq = 2 * total + (int)min(d.ctl->n_outl, d.outl_cap);
+      T.nseq = 2 * total + (T.obkt >= 0 ? (int)T.nout : (int)min(d.ctl->n_outl, d.outl_cap));
     }
   }
   __syncthreads();
@@ -3078,6 +3111,12 @@ __global__ void __launch_bounds__(256, PAIR_WAVES) k_pair_scan(KParams P, Dev d)
   const int x0 = tx * P.tile, y0 = ty * P.tile, w = min(P.tile, P.ncx - x0), h = min(P.tile, P.ncy - y0);
   wg_list_init(Lc);
   wg_list_init(Lr);
+  if (threadIdx.x == 0) {  // this tile's outlier bucket (read before tile_load's first barrier), then reset
+    const uint32_t no = d.tout_n[blockIdx.x];
+    T.nout = no;
+    T.obkt = no <= (uint32_t)P.tout_cap ? (int)blockIdx.x : -1;
+    if (no) d.tout_n[blockIdx.x] = 0;
+  }
   Stamper S(0);
   if (!pair_scan_block(P, d, tile_geo(x0, y0, w, h), T, site, Lc, Lr, S) && threadIdx.x == 0) {
     const uint32_t o = atomicAdd(&d.ctl->n_dense, 1u);  // k_col_exact takes it
@@ -3548,6 +3587,7 @@ __global__ void __launch_bounds__(256) k_finalize(KParams P, Dev d, double time_
   c->last[5] = n_rl;
   c->last[6] = n_cisc;
   c->last[7] = n_ovf;
+  c->last_outl = c->n_outl;
   c->n_overflow = 0;
   c->n_dirty[(step + 1) & 1] = 0;  // consumed by this step's k_cx_kill; the next step's reactions fill it
   c->n_heavy = 0;

@@ -239,6 +239,32 @@ def test_list_overflow_grow_and_replay(monkeypatch, capfd):
     assert replays and replays[-1] > 0, "the lists never overflowed: the replay path was not exercised"
 
 
+@pytest.mark.parametrize("tout_cap", [None, "2", "0"])
+def test_outlier_buckets_without_resort(monkeypatch, capfd, tout_cap):
+    # KMC_RESORT=0: the home cells are never refreshed, so records drift more
+    # than a cell from home and proteins cross the periodic boundary — the
+    # outliers every tile must still stage (kmc_kernels.hip put_rec).  With the
+    # default bucket capacity each tile reads its own bucket; with 2 most
+    # tiles holding outliers overflow it and read the whole outlier list; with
+    # 0 every such tile does.  The trajectory must not change.
+    monkeypatch.setenv("KMC_RESORT", "0")
+    monkeypatch.setenv("KMC_DEBUG_COUNTS", "1")
+    if tout_cap is not None:
+        monkeypatch.setenv("KMC_DEBUG_TOUT_CAP", tout_cap)
+    p = params(seed=43, **DENSE)
+    o = O.Oracle(p)
+    o.init_placement()
+    sim = engine.Simulation(p)
+    sim.set_state(o.get_state())
+    obs = np.concatenate([sim.step(500) for _ in range(4)])
+    obs_o, _ = o.step(2000, want_hashes=False)
+    assert np.array_equal(obs, obs_o)
+    assert engine.state_hash(p, sim.get_state()) == o.hash()
+    import re
+    outl = [int(x) for x in re.findall(r"outliers (\d+)", capfd.readouterr().err)]
+    assert outl and outl[-1] > 10, f"too few outlier records to exercise the buckets: {outl}"
+
+
 def test_threshold_rebuild_without_resort(monkeypatch, capfd):
     # KMC_RESORT=0: no periodic re-sort resets the members[] cursor, so the
     # rows of the kept complexes (appended on every re-registration) reach
