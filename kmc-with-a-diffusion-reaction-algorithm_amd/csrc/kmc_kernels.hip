@@ -2259,16 +2259,21 @@ __device__ __forceinline__ void wg_emit(WgList& L, int2 v, const SList& out, uin
   sl_push(out, v, err);
 }
 
-// all threads of the workgroup
-__device__ __forceinline__ void wg_flush(WgList& L, const SList& out, uint32_t* err) {
+// Two lists of the workgroup at once: both slot reservations (one global
+// atomic each, on threads 0 and 64) are in flight together.  All threads.
+__device__ __forceinline__ void wg_flush2(WgList& L0, const SList& o0, WgList& L1, const SList& o1, uint32_t* err) {
   __syncthreads();
-  const uint32_t m = min(L.n, (uint32_t)EBUF);
+  const uint32_t m0 = min(L0.n, (uint32_t)EBUF), m1 = min(L1.n, (uint32_t)EBUF);
   const int k = my_shard();
-  if (threadIdx.x == 0) L.base = m ? atomicAdd(&out.cnt[k], m) : 0;
+  if (threadIdx.x == 0) L0.base = m0 ? atomicAdd(&o0.cnt[k], m0) : 0;
+  if (threadIdx.x == 64) L1.base = m1 ? atomicAdd(&o1.cnt[k], m1) : 0;
   __syncthreads();
-  const uint32_t base = L.base;
-  for (uint32_t t = threadIdx.x; t < m; t += blockDim.x) {
-    if (base + t < out.cap) out.data[(size_t)k * out.cap + base + t] = L.buf[t];
+  const uint32_t b0 = L0.base, b1 = L1.base;
+  for (uint32_t t = threadIdx.x; t < m0 + m1; t += blockDim.x) {
+    const bool first = t < m0;
+    const uint32_t i = first ? t : t - m0, base = first ? b0 : b1;
+    const SList& out = first ? o0 : o1;
+    if (base + i < out.cap) out.data[(size_t)k * out.cap + base + i] = first ? L0.buf[i] : L1.buf[i];
     else atomicOr(err, ERR_EDGES);
   }
 }
@@ -2300,7 +2305,11 @@ __device__ __forceinline__ void wg_flush(WgList& L, const SList& out, uint32_t* 
 #define NSEG_MAX (2 * HALO_MAX)
 #define HOME_MAX (TILE_MAX + 4)
 #define HSEG_MAX (2 * HOME_MAX)
-#define CFLAT_MAX (NSEG_MAX * (HALO_MAX + 1) + 1)
+#ifndef SUBC  // sub-columns per cell in the LDS bins (x extent of the cut stencils: 130 / SUBC Å steps)
+#define SUBC 2
+#endif
+#define CFLAT_MAX (NSEG_MAX * (HALO_MAX * SUBC + 1) + 1)
+#define SCAN_PER ((CFLAT_MAX + 255) / 256)  // bin counters per thread in the block scans
 #ifndef TCAP
 #define TCAP 640
 #endif
@@ -2330,21 +2339,47 @@ __device__ __forceinline__ TileGeo tile_geo(int x0, int y0, int w, int h) {
   return G;
 }
 
-struct TileLds {
-  float4 pos[TCAP];
-  int2 id[TCAP];                   // {home position | the record's flags, owner key}
-  uint16_t tag[TCAP];              // segment | column << 8 of each staged record's cell
-  int cstart[CFLAT_MAX];           // [seg][hw + 1] flat: record counts, then the LDS index of each cell's
-                                   // first record; [seg][hw] = the segment's end
+// the home headers live only through the staging, the output lists only
+// through the walk and the flush: they share LDS (one more workgroup per CU)
+struct TileHdr {
   int hs[HSEG_MAX][HOME_MAX + 1];  // home segment = home row * 2 + kind: first home position of each column
   int hbase[HSEG_MAX];             // home position − home entry index, per home segment
   int hoff[HSEG_MAX + 1];          // home entries before each home segment; [nhseg] = all
   uint16_t htag[HTAG_MAX];         // home segment | column << 8 of each home entry
+};
+struct TileLists {
+  WgList Lc, Lr;                   // collision candidates, reaction pairs
+};
+struct TileLds {
+  float4 pos[TCAP];
+  int2 id[TCAP];                   // {home position | the record's flags, owner key}
+  uint16_t tag[TCAP];              // segment | column << 8 of each staged record's cell
+  int cstart[CFLAT_MAX];           // [seg][hw · SUBC + 1] flat, bins = (cell column, sub-column): record
+                                   // counts, then the LDS index of each bin's first record; [seg][hw · SUBC]
+                                   // = the segment's end
+  union {
+    TileHdr h;
+    TileLists l;
+  } u;
   int n, nseq, nhome;
   int obkt;                        // the block's outlier bucket (tile index), or -1: the whole outlier list
   uint32_t nout;                   // entries of that bucket
 };
-__device__ __forceinline__ int tcs(const TileLds& T, int hw, int seg, int hx) { return T.cstart[seg * (hw + 1) + hx]; }
+__device__ __forceinline__ int tcs(const TileLds& T, int hw, int seg, int b) { return T.cstart[seg * (hw * SUBC + 1) + b]; }
+// Bin of float x in halo column hx: the block-wide sub-column index
+// (x − x0)·SUBC/cs (float, truncated: monotone in x) clamped into the
+// column's SUBC bins.  Records and cut stencils use the same function, so
+// an x interval maps onto a contiguous run of bins holding every record in it.
+struct SubCol {
+  float x0, k;  // the halo region's left edge, SUBC / cs
+};
+__device__ __forceinline__ SubCol sub_cols(const KParams& P, const TileGeo& G) {
+  return SubCol{(float)(P.gx0 + G.cx0 * P.cs), (float)(SUBC / P.cs)};
+}
+__device__ __forceinline__ int sub_bin(const SubCol& C, int hx, float x) {
+  const int g = (int)((x - C.x0) * C.k);
+  return min(max(g, hx * SUBC), hx * SUBC + SUBC - 1);
+}
 
 // global record index of staged record l (record w of home position hp at 2·hp + w)
 __device__ __forceinline__ int tile_global(const TileLds& T, int l) {
@@ -2352,15 +2387,14 @@ __device__ __forceinline__ int tile_global(const TileLds& T, int l) {
   return 2 * (x & RID_PID) + (x < 0 ? 1 : 0);
 }
 
-// exclusive prefix sum of a[0..m) in LDS by the whole workgroup (m <= 4·blockDim)
+// exclusive prefix sum of a[0..m) in LDS by the whole workgroup (m <= SCAN_PER·blockDim)
 __device__ __forceinline__ int block_excl_scan(int* a, int m, int* wtot) {
   const int t = threadIdx.x, lane = __lane_id(), w = t >> 6, nw = blockDim.x >> 6;
-  int v[4], sum = 0;
+  int sum = 0;  // (each thread's own entries are read again below: no register array)
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int i = 4 * t + k;
-    v[k] = i < m ? a[i] : 0;
-    sum += v[k];
+  for (int k = 0; k < SCAN_PER; ++k) {
+    const int i = SCAN_PER * t + k;
+    sum += i < m ? a[i] : 0;
   }
   int inc = sum;
 #pragma unroll
@@ -2377,10 +2411,13 @@ __device__ __forceinline__ int block_excl_scan(int* a, int m, int* wtot) {
   }
   int run = base + inc - sum;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int i = 4 * t + k;
-    if (i < m) a[i] = run;
-    run += v[k];
+  for (int k = 0; k < SCAN_PER; ++k) {
+    const int i = SCAN_PER * t + k;
+    if (i < m) {
+      const int x = a[i];
+      a[i] = run;
+      run += x;
+    }
   }
   __syncthreads();
   return tot;
@@ -2397,24 +2434,24 @@ __device__ __forceinline__ int tile_elem(const Dev& d, const TileLds& T, const T
     const int e = q >> 1, w = q & 1;
     int seg, hx;
     if (nhome <= HTAG_MAX) {
-      const int tg = T.htag[e];
+      const int tg = T.u.h.htag[e];
       seg = tg & 0xff;
       hx = tg >> 8;
     } else {  // more home entries than tags: search the segment, then the column
       seg = 0;
 #pragma unroll
       for (int st = 32; st; st >>= 1)
-        if (seg + st <= G.nhseg - 1 && T.hoff[seg + st] <= e) seg += st;
-      const int hp = T.hbase[seg] + e;
+        if (seg + st <= G.nhseg - 1 && T.u.h.hoff[seg + st] <= e) seg += st;
+      const int hp = T.u.h.hbase[seg] + e;
       hx = 0;
 #pragma unroll
       for (int st = 16; st; st >>= 1)
-        if (hx + st <= G.mw - 1 && T.hs[seg][hx + st] <= hp) hx += st;
+        if (hx + st <= G.mw - 1 && T.u.h.hs[seg][hx + st] <= hp) hx += st;
     }
     ax = G.hx0 + hx;
     ay = G.hy0 + (seg >> 1);
     kind = seg & 1;
-    return 2 * (T.hbase[seg] + e) + w;
+    return 2 * (T.u.h.hbase[seg] + e) + w;
   }
   if (T.obkt >= 0) {
     const int2 o = d.tout[(size_t)T.obkt * TOUT_CAP + (q - 2 * nhome)];
@@ -2435,7 +2472,8 @@ __device__ __forceinline__ int tile_elem(const Dev& d, const TileLds& T, const T
 // for the brute-force path).
 __device__ bool tile_load(const KParams& P, const Dev& d, const TileGeo& G, TileLds& T, float2* site, Stamper& S) {
   const int hw = G.hw, hh = G.hh, mw = G.mw, nhseg = G.nhseg;
-  const int nflat = 2 * hh * (hw + 1) + 1;
+  const int nflat = 2 * hh * (hw * SUBC + 1) + 1;
+  const SubCol SC = sub_cols(P, G);
   __shared__ int wtot[16];
 #ifndef HDR_WAVE
   {  // home segment heads, every load in flight before the stores; cell counters zeroed
@@ -2455,7 +2493,7 @@ __device__ bool tile_load(const KParams& P, const Dev& d, const TileGeo& G, Tile
     for (int k = 0; k < NH; ++k) {
       const int idx = threadIdx.x + k * (int)blockDim.x;
       const int seg = idx / (mw + 1), hx = idx - seg * (mw + 1);
-      if (seg < nhseg) T.hs[seg][hx] = v[k];
+      if (seg < nhseg) T.u.h.hs[seg][hx] = v[k];
     }
     for (int idx = threadIdx.x; idx < nflat; idx += blockDim.x) T.cstart[idx] = 0;
   }
@@ -2469,7 +2507,7 @@ __device__ bool tile_load(const KParams& P, const Dev& d, const TileGeo& G, Tile
         int v = 0;
         if (y >= 0 && y < P.ncy && xlo <= xhi)
           v = d.hstart[cell_index(P, min(max(G.hx0 + lane, xlo), xhi + 1), y, seg & 1)];
-        T.hs[seg][lane] = v;
+        T.u.h.hs[seg][lane] = v;
       }
     }
     for (int idx = threadIdx.x; idx < nflat; idx += blockDim.x) T.cstart[idx] = 0;
@@ -2479,7 +2517,7 @@ __device__ bool tile_load(const KParams& P, const Dev& d, const TileGeo& G, Tile
   S(d, 0);
   if (threadIdx.x < 64) {  // home segment lengths -> entries before each segment
     const int seg = threadIdx.x;
-    const int len = seg < nhseg ? T.hs[seg][mw] - T.hs[seg][0] : 0;
+    const int len = seg < nhseg ? T.u.h.hs[seg][mw] - T.u.h.hs[seg][0] : 0;
     int inc = len;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -2487,8 +2525,8 @@ __device__ bool tile_load(const KParams& P, const Dev& d, const TileGeo& G, Tile
       if (seg >= o) inc += t;
     }
     const int total = __shfl(inc, 63, 64);
-    if (seg <= nhseg) T.hoff[seg] = inc - len;
-    if (seg < nhseg) T.hbase[seg] = T.hs[seg][0] - (inc - len);
+    if (seg <= nhseg) T.u.h.hoff[seg] = inc - len;
+    if (seg < nhseg) T.u.h.hbase[seg] = T.u.h.hs[seg][0] - (inc - len);
     if (seg == 0) {
       T.nhome = total;
       T.nseq = 2 * total + (T.obkt >= 0 ? (int)T.nout : (int)min(d.ctl->n_outl, d.outl_cap));
@@ -2498,8 +2536,8 @@ __device__ bool tile_load(const KParams& P, const Dev& d, const TileGeo& G, Tile
   if (T.nhome <= HTAG_MAX)  // home entry -> (segment, column) tags, one thread per home cell
     for (int idx = threadIdx.x; idx < nhseg * mw; idx += blockDim.x) {
       const int seg = idx / mw, hx = idx - seg * mw;
-      const int e0 = T.hoff[seg] + (T.hs[seg][hx] - T.hs[seg][0]), e1 = e0 + (T.hs[seg][hx + 1] - T.hs[seg][hx]);
-      for (int e = e0; e < e1; ++e) T.htag[e] = (uint16_t)(seg | hx << 8);
+      const int e0 = T.u.h.hoff[seg] + (T.u.h.hs[seg][hx] - T.u.h.hs[seg][0]), e1 = e0 + (T.u.h.hs[seg][hx + 1] - T.u.h.hs[seg][hx]);
+      for (int e = e0; e < e1; ++e) T.u.h.htag[e] = (uint16_t)(seg | hx << 8);
     }
   __syncthreads();
   S(d, 1);
@@ -2525,6 +2563,7 @@ __device__ bool tile_load(const KParams& P, const Dev& d, const TileGeo& G, Tile
       if (gi[k] >= 0) rr[k] = d.rec[gi[k]];
 #pragma unroll
     for (int k = 0; k < NE; ++k) {
+      const float xr = rr[k].pos.x;
       cell[k] = -1;
       if (gi[k] < 0) continue;
       int x = ax[k], y = ay[k];
@@ -2537,7 +2576,8 @@ __device__ bool tile_load(const KParams& P, const Dev& d, const TileGeo& G, Tile
       const int hx = x - G.cx0, hy = y - G.cy0;
       if (hx < 0 || hx >= hw || hy < 0 || hy >= hh) continue;
       const int kind = (rr[k].id.x & RID_LIG) ? 1 : 0, seg = hy * 2 + kind;
-      cell[k] = (seg * (hw + 1) + hx) | (seg | hx << 8) << 16;  // flat cell | LDS tag << 16
+      const int b = sub_bin(SC, hx, xr);
+      cell[k] = (seg * (hw * SUBC + 1) + b) | (seg | hx << 8) << 16;  // flat bin | LDS tag << 16
     }
   };
   auto count = [&]() {
@@ -2581,16 +2621,16 @@ __device__ bool tile_load(const KParams& P, const Dev& d, const TileGeo& G, Tile
         if (cell[k] >= 0) place(k, atomicAdd(&T.cstart[cell[k] & 0xffff], 1));
     }
     __syncthreads();
-    int v[4];
+    int v[SCAN_PER];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int i = 4 * (int)threadIdx.x + k;
+    for (int k = 0; k < SCAN_PER; ++k) {
+      const int i = SCAN_PER * (int)threadIdx.x + k;
       v[k] = i >= 1 && i < nflat ? T.cstart[i - 1] : 0;
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int i = 4 * (int)threadIdx.x + k;
+    for (int k = 0; k < SCAN_PER; ++k) {
+      const int i = SCAN_PER * (int)threadIdx.x + k;
       if (i < nflat) T.cstart[i] = v[k];
     }
   }
@@ -2608,13 +2648,18 @@ __device__ __forceinline__ void item_ranges(const KParams& P, const TileLds& T, 
   const int cx = G.cx0 + hx, cy = G.cy0 + hy;
   const float xb = (float)(P.gx0 + cx * P.cs), yb = (float)(P.gy0 + cy * P.cs), cs = (float)P.cs;
   const int lo = hx - (px - xb < reach ? 1 : 0), hi = hx + (xb + cs - px < reach ? 1 : 0);
+  // bins from the sub-column of px − reach in the first cell to that of
+  // px + reach in the last (sub_col is monotone: every record within reach
+  // of px in x lies in between)
+  const SubCol SC = sub_cols(P, G);
+  const int blo = sub_bin(SC, lo, px - reach), bhi = sub_bin(SC, hi, px + reach);
   const bool down = py - yb < reach, up = yb + cs - py < reach;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     const int s = (hy - 1 + k) * 2 + kind;
     const bool on = k == 1 || (k == 0 ? down : up);
-    r0[k] = on ? tcs(T, G.hw, s, lo) : 0;
-    r1[k] = on ? tcs(T, G.hw, s, hi + 1) : 0;
+    r0[k] = on ? tcs(T, G.hw, s, blo) : 0;
+    r1[k] = on ? tcs(T, G.hw, s, bhi + 1) : 0;
   }
 }
 
@@ -2627,11 +2672,24 @@ __device__ __forceinline__ void item_ranges(const KParams& P, const TileLds& T, 
 // every lane checks a pair, the owner's record is a broadcast LDS read and the
 // neighbour records of consecutive lanes are mostly consecutive.
 // chk(l, r) for every pair; all threads call (no barrier).
+#ifndef WALK_STRIDE  // (A/B builds: 0 = each wave takes 64 consecutive records)
+#define WALK_STRIDE 1
+#endif
 template <class Rng, class Chk>
 __device__ __forceinline__ void tile_walk(const TileGeo& G, const TileLds& T, Rng rng, Chk chk) {
   const int n = T.n, lane = __lane_id();
+  // records go to the waves round-robin (record base + lane·nw + wave): the
+  // staged records are in bin order, so each wave samples the whole block and
+  // the waves of a workgroup walk about the same number of pairs
+#if WALK_STRIDE
+  const int nw = blockDim.x >> 6, wv = threadIdx.x >> 6;
+#endif
   for (int base = 0; base < n; base += blockDim.x) {
+#if WALK_STRIDE
+    const int l = base + lane * nw + wv;
+#else
     const int l = base + threadIdx.x;
+#endif
     int r0[6], r1[6];
     bool item = false;
     if (l < n) {
@@ -2654,7 +2712,9 @@ __device__ __forceinline__ void tile_walk(const TileGeo& G, const TileLds& T, Rn
       if (lane >= o) inc += t;
     }
     const int excl = inc - tot, wtot = __shfl(inc, 63, 64);
+#if !WALK_STRIDE
     const int l0 = l - lane;
+#endif
     for (int j = 0; j < wtot; j += 64) {
       const int q = j + lane;
       int o = 0;  // owner: the number of lanes whose inclusive prefix is <= q
@@ -2669,7 +2729,11 @@ __device__ __forceinline__ void tile_walk(const TileGeo& G, const TileLds& T, Rn
         const uint32_t v = __shfl(pk[k], o, 64);
         if ((int)(v >> 16) <= t) sel = v;
       }
+#if WALK_STRIDE
+      if (q < wtot) chk(base + o * nw + wv, (int)(sel & 0xffffu) + t - (int)(sel >> 16));
+#else
       if (q < wtot) chk(l0 + o, (int)(sel & 0xffffu) + t - (int)(sel >> 16));
+#endif
     }
   }
 }
@@ -3042,7 +3106,10 @@ __device__ __forceinline__ void rxn_emit(const Dev& d, WgList& L, int a, int b) 
 __device__ __forceinline__ bool pair_scan_block(const KParams& P, const Dev& d, const TileGeo& G, TileLds& T,
                                                 float2* site, WgList& Lc, WgList& Lr, Stamper& S) {
   const int NB = P.NB;
-  if (!tile_load(P, d, G, T, site, S)) return false;
+  const bool staged = tile_load(P, d, G, T, site, S);
+  wg_list_init(Lc);  // (the lists share LDS with the home headers: after the staging)
+  wg_list_init(Lr);
+  if (!staged) return false;
   if (P.dbg_stage == 1) return true;
   PairBuf Bc, Br;
   Bc.n = 0;
@@ -3105,12 +3172,11 @@ __device__ __forceinline__ bool pair_scan_block(const KParams& P, const Dev& d, 
 __global__ void __launch_bounds__(256, PAIR_WAVES) k_pair_scan(KParams P, Dev d) {
   __shared__ TileLds T;
   __shared__ float2 site[TCAP];
-  __shared__ WgList Lc, Lr;
+  WgList& Lc = T.u.l.Lc;
+  WgList& Lr = T.u.l.Lr;
   const int ntx = (P.ncx + P.tile - 1) / P.tile;
   const int tx = blockIdx.x % ntx, ty = blockIdx.x / ntx;
   const int x0 = tx * P.tile, y0 = ty * P.tile, w = min(P.tile, P.ncx - x0), h = min(P.tile, P.ncy - y0);
-  wg_list_init(Lc);
-  wg_list_init(Lr);
   if (threadIdx.x == 0) {  // this tile's outlier bucket (read before tile_load's first barrier), then reset
     const uint32_t no = d.tout_n[blockIdx.x];
     T.nout = no;
@@ -3124,8 +3190,7 @@ __global__ void __launch_bounds__(256, PAIR_WAVES) k_pair_scan(KParams P, Dev d)
     else atomicOr(&d.ctl->err, ERR_EDGES);
   }
   if (P.dbg_stage == 1 || P.dbg_stage == 3) return;
-  wg_flush(Lc, d.cand, &d.ctl->err);
-  wg_flush(Lr, d.pairs, &d.ctl->err);
+  wg_flush2(Lc, d.cand, Lr, d.pairs, &d.ctl->err);
   S(d, 7);
 }
 
