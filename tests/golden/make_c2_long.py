@@ -18,10 +18,20 @@ the result is data only.  The file is rewritten
 (atomically) every SAVE_EVERY steps with the steps done so far, so a long run
 (BASELINE.json C2: 10^5 steps) yields a usable, shorter fixture at any time.
 
-Usage: python tests/golden/make_c2_long.py [steps] [out]
+Segments (10^5 steps in parallel, VERDICT r03 "next" 5):
+  make_c2_long.py STEPS OUT --start-state S.kst --save-state E.kst
+starts the oracle from the exact state S (KMCSTAT1, its step is the segment's
+first step), advances it STEPS steps and saves its own exact final state E.
+tests/golden/merge_c2_segments.py joins segments into one fixture, and accepts
+a join only when the earlier segment's own final state is byte-identical to the
+state the next segment started from, so every step of the joined fixture is
+the oracle's and the joined run is the one continuous oracle run.
+
+Usage: python tests/golden/make_c2_long.py [steps] [out] [--start-state S] [--save-state E]
 """
 from __future__ import annotations
 
+import argparse
 import os
 import sys
 import time
@@ -45,10 +55,16 @@ OUT = os.path.join(HERE, "c2_long.npz")
 
 
 def main():
-    steps = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
-    out = sys.argv[2] if len(sys.argv) > 2 else OUT
+    ap = argparse.ArgumentParser()
+    ap.add_argument("steps", type=int, nargs="?", default=10000)
+    ap.add_argument("out", nargs="?", default=OUT)
+    ap.add_argument("--start-state", default="")
+    ap.add_argument("--save-state", default="")
+    a = ap.parse_args()
+    steps, out = a.steps, a.out
     p = workloads.params("C2", seed=1)
-    st = engine.host_init_random(p)
+    st = engine.host_load_state(p, a.start_state) if a.start_state else engine.host_init_random(p)
+    start = int(st.step)
     o = O.Oracle(p, rng_mode=O.RNG_KEYED, nbmode=O.NB_CELLS)
     o.set_state(st)
     obs = np.zeros(steps, dtype=O.capi.OBS_DTYPE)
@@ -58,7 +74,7 @@ def main():
     def save(done):
         tmp = out + ".tmp.npz"
         np.savez_compressed(tmp, obs=obs[:done], hashes=hashes[:done // HASH_EVERY], steps=done,
-                            hash_every=HASH_EVERY, seed=1,
+                            hash_every=HASH_EVERY, seed=1, start=start,
                             events=np.array(list(o.stats().values()), dtype=np.int64))
         os.replace(tmp, out)
         print("wrote", out, done, o.stats(), flush=True)
@@ -69,10 +85,13 @@ def main():
         hashes[c] = o.hash()
         done = (c + 1) * HASH_EVERY
         if c % 10 == 9:
-            print(f"step {done} bonds {ob[-1]['bond_num']} rl {ob[-1]['bond_num_rl']} "
+            print(f"step {start + done} bonds {ob[-1]['bond_num']} rl {ob[-1]['bond_num_rl']} "
                   f"{time.time() - t0:.0f}s", flush=True)
         if done % SAVE_EVERY == 0 or done == steps:
             save(done)
+    if a.save_state:
+        engine.host_save_state(p, o.get_state(), a.save_state)
+        print("saved", a.save_state, "step", o.current_step, flush=True)
 
 
 if __name__ == "__main__":
