@@ -135,11 +135,19 @@ def visible_devices() -> int:
         return 0
 
 
+def shared_device() -> bool:
+    """KMC_BENCH_SHARED_DEVICE=1 (tests only): every rank on device 0 and the
+    gloo backend, so the N-rank path (launcher, rendezvous, max over ranks,
+    ensemble reduction) runs on a one-GPU box (tests/test_gpu_bench_ranks.py).
+    The line then says so in ensemble_reduce.shared_device."""
+    return os.environ.get("KMC_BENCH_SHARED_DEVICE") == "1"
+
+
 def launch(args, argv) -> int:
     n = args.gpus
     if not args.launcher_check:
         ndev = visible_devices()
-        if ndev < n:
+        if ndev < (1 if shared_device() else n):
             print(f"bench.py: --gpus {n} needs {n} visible GPUs, found {ndev}; refusing to measure fewer",
                   file=sys.stderr, flush=True)
             return 2
@@ -212,15 +220,20 @@ def run_rank(args, rank: int, world: int, local: int):
 
     # RCCL (backend "nccl") at every world size: at N = 1 the ensemble
     # reduction below runs the same device-tensor all-reduce path as on 8 GPUs
+    shared = shared_device()
+    if shared:
+        local = 0
     torch.cuda.set_device(local)
-    if world == 1 and "MASTER_ADDR" not in os.environ:
+    if shared:
+        dist.init_process_group("gloo")
+    elif world == 1 and "MASTER_ADDR" not in os.environ:
         dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
                                 device_id=torch.device("cuda", local))
     else:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     if dist.get_world_size() != world:
         sys.exit(f"bench.py: process group has {dist.get_world_size()} ranks, expected {world}")
-    if world > 1:
+    if world > 1 and not shared:
         props = torch.cuda.get_device_properties(local)
         me = str(getattr(props, "uuid", "")) or f"{props.name}:{local}"
         devs = [None] * world
@@ -250,14 +263,19 @@ def run_rank(args, rank: int, world: int, local: int):
 
     last_obs = {}
 
+    reducer = ensemble.Reducer(args.steps, device=None if shared else dev)
+
     def timed(k):
         barrier()
         t = time.perf_counter()
         obs = sim.step(k)
-        red = ensemble.reduce(obs, device=dev)
+        t_steps = time.perf_counter()
+        red = reducer.reduce(obs)
         barrier()
+        t_end = time.perf_counter()
         last_obs["obs"] = obs
-        return time.perf_counter() - t, red
+        last_obs["split_ms"] = {"steps": (t_steps - t) * 1e3, "reduce_and_barrier": (t_end - t_steps) * 1e3}
+        return t_end - t, red
 
     def max_over_ranks(x):
         if world == 1:
@@ -304,7 +322,8 @@ def run_rank(args, rank: int, world: int, local: int):
     # what the all-reduce did: at N = 1 the reduced series must equal this
     # rank's own observables (the same RCCL call the N-GPU run makes)
     own_s, own_m = ensemble.pack(last_obs["obs"])
-    reduce_info = {"backend": dist.get_backend(), "device": str(dev), "world": world,
+    reduce_info = {"backend": dist.get_backend(), "device": "cpu" if shared else str(dev), "world": world,
+                   "shared_device": shared,
                    "ops": ["all_reduce SUM int64[K,6]", "all_reduce MAX int64[K,1]"], "steps_reduced": args.steps}
     if world == 1:
         reduce_info["equals_local"] = bool((sums == own_s).all() and (maxima == own_m).all())
@@ -353,6 +372,7 @@ def run_rank(args, rank: int, world: int, local: int):
                 "timed_from_step": sim.current_step - args.steps,
                 "ms_per_step_fresh": fresh_ms,
                 "per_rank_ms_per_step": [x / args.steps * 1e3 for x in per_rank],
+                "window_split_ms": last_obs["split_ms"],
                 "efficiency_vs_rank0": per_rank[0] / dt,
                 "final_bond_num_ensemble": int(sums[-1, 3]),
                 "final_rl_ensemble": int(sums[-1, 0]),

@@ -35,6 +35,8 @@ struct KParams {
   int cx_serial;  // debug: complexes aligned by one lane (KMC_CX_SERIAL=1) instead of the whole wave
   uint32_t cx_limit;  // members[] cursor above which k_finalize latches a full complex rebuild (mcap / 2;
                       // lowered only by KMC_DEBUG_CX_LIMIT to exercise the rebuild)
+  int htag_max;   // tile home entries tagged for the direct lookup (<= HTAG_MAX; lowered only by KMC_DEBUG_HTAG)
+  int dbg_recs;   // debug (KMC_DEBUG_RECS=1): every record stamped with its step and checked before the pair scan
 };
 
 // per-step control block in device memory (replayable without host writes)

@@ -49,11 +49,17 @@ struct kmc_sim {
   // output-list capacities: 2^grow times the initial sizes; kmc_step doubles
   // them and replays the chunk when a list overflows (ERR_EDGES)
   int grow = 0;
-  // chunk snapshot for the replay: R, state rows, slot maps, control block
+  // snapshot for the replay: R, state rows, slot maps, control block.  Taken
+  // lazily: a kmc_step chunk reuses the last snapshot while it is at most
+  // snap_span steps behind the chunk's end (keyed draws: replaying the steps
+  // since the snapshot reproduces them), so short kmc_step calls do not each
+  // copy the whole state (KMC_SNAP_SPAN=0: a snapshot per chunk)
   double *snap_a = nullptr, *snap_b = nullptr;
   int32_t *snap_ai = nullptr, *snap_bi = nullptr, *snap_id = nullptr, *snap_slot = nullptr;
   Ctl* snap_ctl = nullptr;
-  int64_t n_replays = 0;
+  bool snap_valid = false;
+  int64_t snap_step = 0, snap_since = 0, snap_span = 4096;
+  int64_t n_replays = 0, n_snapshots = 0;
   // complexes are kept across steps (k_cx_kill); full: register every one anew
   // at the next step (set after a new state, a re-sort is handled per step, an
   // undone chunk); KMC_FULL_BFS=1: every step
@@ -376,8 +382,9 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   {
     const double rho = (double)N * K.cs * K.cs / std::max(1.0, p->box_x * p->box_y);  // proteins per cell
     int t = TILE_MAX;
-    // (a block whose records still overflow TCAP is split into quarters by
-    // k_pair_scan itself: the bound below keeps that rare)
+    // (a tile whose records still overflow TCAP goes onto the dense list and
+    // is brute-forced from global memory by k_col_exact: the mean is kept at
+    // 0.75 TCAP, > 7 Poisson sigmas below TCAP at the benchmark densities)
     while (t > 4 && (t * t * rho > 205.0 || (t + 2) * (t + 2) * 2.0 * rho > 0.75 * TCAP)) --t;
     const char* te = getenv("KMC_TILE");
     if (te && *te) t = std::max(2, std::min(TILE_MAX, atoi(te)));
@@ -390,6 +397,17 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
     K.cx_serial = cxs && *cxs == '1';
     const char* gr = getenv("KMC_GRAPH");
     s->use_graphs = gr && *gr == '1';
+    const char* ht = getenv("KMC_DEBUG_HTAG");  // debug: fewer tagged home entries (the searched lookup)
+    K.htag_max = HTAG_MAX;
+    if (ht && *ht) K.htag_max = std::max(0, std::min(HTAG_MAX, atoi(ht)));
+    const char* dr = getenv("KMC_DEBUG_RECS");
+    K.dbg_recs = dr && *dr == '1';
+    if (K.dbg_recs && dalloc(s, &d.rec_step, 2 * (size_t)N) != KMC_OK) {
+      kmc_destroy(s);
+      return KMC_ERR_HIP;
+    }
+    const char* sp = getenv("KMC_SNAP_SPAN");
+    if (sp && *sp) s->snap_span = std::max<int64_t>(0, atoll(sp));
   }
   {
     const uint64_t kmax = (uint64_t)K.ncx * K.ncy;  // row-major cell keys (k_slot_keys)
@@ -629,6 +647,7 @@ int kmc_set_state(kmc_sim* s, const kmc_state_view* v) {
   s->have_state = true;
   s->need_full = true;
   s->clusters_valid = false;
+  s->snap_valid = false;
   return KMC_OK;
 }
 
@@ -800,6 +819,7 @@ static int launch_step(kmc_sim* s, bool re_sort) {
       TIMED(KI_CX_HEAVY, (k_complex_heavy<<<1024, T, 0, st>>>(K, d)));
     }
   }
+  if (K.dbg_recs) k_rec_check<<<std::min(2048, (2 * K.N + T - 1) / T), T, 0, st>>>(K, d);
   const int gX = std::min(2048, (K.N + T - 1) / T);  // grid-stride kernels over device-sized lists
   const int ntiles = s->ntiles;
   // collision candidates and reaction candidates, one staging of each tile
@@ -893,8 +913,10 @@ static int run_chunk(kmc_sim* s, int64_t n) {
 }
 
 // Steps run in chunks of up to 4096 launched back to back; the device error
-// bits are read once per chunk.  Every chunk starts from a device snapshot of
-// its initial state, so a chunk that raised an error bit is undone:
+// bits are read once per chunk.  A device snapshot of the state at most
+// snap_span steps before the chunk's end is kept (taken at a chunk start when
+// the last one is older), so a chunk that raised an error bit is undone by
+// restoring it and replaying the steps between it and the chunk:
 //  * an output list or edge buffer overflowed (ERR_EDGES): the lists are
 //    doubled and the chunk replayed — with keyed draws the replay is the same
 //    trajectory, so capacities never change results;
@@ -916,9 +938,15 @@ int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out) {
   int64_t done = 0;
   while (done < nsteps) {
     const int64_t n = std::min(chunk, nsteps - done);
-    int rc = snapshot(s, false);
-    if (rc != KMC_OK) return rc;
-    const int64_t since0 = s->since_resort;
+    int rc = KMC_OK;
+    if (!s->snap_valid || s->step_done + n - s->snap_step > s->snap_span) {
+      rc = snapshot(s, false);
+      if (rc != KMC_OK) return rc;
+      s->snap_valid = true;
+      s->snap_step = s->step_done;
+      s->snap_since = s->since_resort;
+      ++s->n_snapshots;
+    }
     for (;;) {
       rc = run_chunk(s, n);
       if (rc != KMC_OK) return rc;
@@ -928,16 +956,32 @@ int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out) {
       // dropped entries, so their bits may be consequences
       const uint32_t cause = s->ctl_host->err_first;
       const int64_t bad = (int64_t)s->ctl_host->err_step;
+      // undo to the snapshot, then replay the steps between it and this
+      // chunk (already returned by earlier calls: same trajectory, keyed
+      // draws) without output
       rc = snapshot(s, true);
       if (rc != KMC_OK) return rc;
-      s->since_resort = since0;
+      s->since_resort = s->snap_since;
       s->need_full = true;  // the kept complexes may describe the undone steps
       ++s->n_replays;
-      if ((cause & ERR_EDGES) && s->grow < 6) {  // at most 64x the default lists
+      // a list overflow alone: double the lists (at most 64x the defaults)
+      // and run the chunk again; any other bit is reported at once
+      const bool grow = (cause & ~ERR_EDGES) == 0 && s->grow < 6;
+      if (grow) {
         s->grow += 1;
         if (alloc_lists(s) != KMC_OK) return fail(s, KMC_ERR_HIP, "growing the output lists failed");
-        continue;
       }
+      for (int64_t at = s->snap_step; at < s->step_done;) {
+        const int64_t m = std::min(chunk, s->step_done - at);
+        rc = run_chunk(s, m);
+        if (rc != KMC_OK) return rc;
+        if (s->ctl_host->err) {
+          s->snap_valid = false;
+          return fail(s, KMC_ERR_HIP, "replay from the snapshot raised an error the original steps did not");
+        }
+        at += m;
+      }
+      if (grow) continue;
       // keep the steps before the failing one
       const int64_t good = std::max<int64_t>(0, std::min<int64_t>(n, bad - (s->step_done + 1)));
       if (good > 0) {
@@ -960,9 +1004,9 @@ int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out) {
     s->clusters_valid = true;
     if (s->debug_counts) {
       const uint32_t* l = s->ctl_host->last;
-      fprintf(stderr, "kmc step %lld: candidates %u conflicts %u pending-units %u rejected %u rxn-pairs %u rl-edges %u cis-edges %u bfs-overflow %u outliers %u (list growth 2^%d, replays %lld, forced rebuilds %u)\n",
+      fprintf(stderr, "kmc step %lld: candidates %u conflicts %u pending-units %u rejected %u rxn-pairs %u rl-edges %u cis-edges %u bfs-overflow %u outliers %u (list growth 2^%d, replays %lld, snapshots %lld, forced rebuilds %u)\n",
               (long long)s->step_done, l[0], l[1], l[2], l[3], l[4], l[5], l[6], l[7], s->ctl_host->last_outl, s->grow,
-              (long long)s->n_replays, s->ctl_host->n_forced);
+              (long long)s->n_replays, (long long)s->n_snapshots, s->ctl_host->n_forced);
       const uint64_t* t = s->ctl_host->stamps;
       if (t[16])
         fprintf(stderr, "kmc stamps cx stage %llu rigid %llu checks %llu writeback %llu count %llu next %llu\n",

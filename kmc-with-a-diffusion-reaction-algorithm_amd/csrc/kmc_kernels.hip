@@ -82,7 +82,9 @@ struct Dev {
   int2* tout;           // [ntiles][TOUT_CAP] the outliers whose cell lies in a pair-scan tile's block + halo:
                         //   {record, cx | cy << 16}
   uint32_t* tout_n;     // [ntiles] entries of each tile's bucket this step (zeroed by the tile's k_pair_scan)
-  int4* dense;          // [dense_cap] blocks of cells whose records overflow the pair scan's LDS: {x0, y0, w, h}
+  uint32_t* rec_step;   // [2N] debug (KMC_DEBUG_RECS): the step each record was last written in
+  int4* dense;          // [dense_cap] tiles whose records overflow the pair scan's LDS: {x0 | y0 << 16,
+                        // w | h << 16, the tile's outlier bucket or -1 (the whole outlier list), its entries}
   uint32_t dense_cap;
   SList cand;           // collision candidates (proposal record, other record)
   SList conf;           // conflict entries (u, kq | isnew<<31)
@@ -601,6 +603,19 @@ __device__ __forceinline__ void put_rec(const KParams& P, const Dev& d, uint2 h,
   r.id = make_int2(p | (p >= P.NA ? RID_LIG : 0) | code << RID_CODE_SHIFT | st | (w << 31), own);
   r.site = make_float2((float)sx, (float)sy);
   d.rec[ri] = r;
+  if (P.dbg_recs) d.rec_step[ri] = d.ctl->step;
+}
+
+// debug (KMC_DEBUG_RECS=1), after the proposal phase: every protein's two
+// records must have been written this step by the kernel that moved it (the
+// pair scan reads them in place; a record left from an earlier step would
+// pair stale positions silently)
+__global__ void k_rec_check(KParams P, Dev d) {
+  const uint32_t step = d.ctl->step;
+  bool bad = false;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < 2 * P.N; i += gridDim.x * blockDim.x)
+    bad |= d.rec_step[i] != step;
+  if (__ballot(bad) && __lane_id() == 0) atomicOr(&d.ctl->err, ERR_RESOLVE);
 }
 
 // status bits of slot p's records
@@ -2294,10 +2309,9 @@ __device__ __forceinline__ void wg_flush2(WgList& L0, const SList& o0, WgList& L
 // neighbour kind, only the cells within that kind pair's reach of the record
 // (its offset inside its cell decides which side columns / rows can hold a
 // partner) — as six LDS index ranges, and each wave walks its records' pairs
-// with every lane busy (tile_walk).  A block whose records do not fit in
-// TCAP is split into quarters (down to single cells), each staged the same
-// way; only a single cell that still does not fit takes the brute-force
-// global-memory path.
+// with every lane busy (tile_walk).  A tile whose records do not fit in
+// TCAP goes onto the dense list: k_col_exact brute-forces it from global
+// memory (its home records and its outlier bucket, dense_block).
 #ifndef TILE_MAX  // (overridable for tile-size sweeps: tools/build_variants.py)
 #define TILE_MAX 14
 #endif
@@ -2347,8 +2361,10 @@ struct TileHdr {
   int hoff[HSEG_MAX + 1];          // home entries before each home segment; [nhseg] = all
   uint16_t htag[HTAG_MAX];         // home segment | column << 8 of each home entry
 };
+#define WALK_WIN 32  // words of each wave's start bitmap in the pair walk (a window of 1024 pairs)
 struct TileLists {
   WgList Lc, Lr;                   // collision candidates, reaction pairs
+  alignas(8) uint32_t wbits[4 * WALK_WIN];  // the pair walk's start bitmaps, one per wave (tile_walk)
 };
 struct TileLds {
   float4 pos[TCAP];
@@ -2427,13 +2443,13 @@ __device__ __forceinline__ int block_excl_scan(int* a, int m, int* wtot) {
 // entry, segment by segment) then the outlier list.  Returns the global
 // record index, with the home cell (home records, kind >= 0) or the record's
 // own cell (outliers, kind = -1).
-__device__ __forceinline__ int tile_elem(const Dev& d, const TileLds& T, const TileGeo& G, int q, int& ax, int& ay,
+__device__ __forceinline__ int tile_elem(const KParams& P, const Dev& d, const TileLds& T, const TileGeo& G, int q, int& ax, int& ay,
                                          int& kind) {
   const int nhome = T.nhome;
   if (q < 2 * nhome) {
     const int e = q >> 1, w = q & 1;
     int seg, hx;
-    if (nhome <= HTAG_MAX) {
+    if (nhome <= P.htag_max) {
       const int tg = T.u.h.htag[e];
       seg = tg & 0xff;
       hx = tg >> 8;
@@ -2533,7 +2549,7 @@ __device__ bool tile_load(const KParams& P, const Dev& d, const TileGeo& G, Tile
     }
   }
   __syncthreads();
-  if (T.nhome <= HTAG_MAX)  // home entry -> (segment, column) tags, one thread per home cell
+  if (T.nhome <= P.htag_max)  // home entry -> (segment, column) tags, one thread per home cell
     for (int idx = threadIdx.x; idx < nhseg * mw; idx += blockDim.x) {
       const int seg = idx / mw, hx = idx - seg * mw;
       const int e0 = T.u.h.hoff[seg] + (T.u.h.hs[seg][hx] - T.u.h.hs[seg][0]), e1 = e0 + (T.u.h.hs[seg][hx + 1] - T.u.h.hs[seg][hx]);
@@ -2547,7 +2563,8 @@ __device__ bool tile_load(const KParams& P, const Dev& d, const TileGeo& G, Tile
 #endif
   constexpr int NE = STAGE_NE;  // elements per thread in flight
   const bool one = nseq <= NE * (int)blockDim.x;  // every element held in registers through the binning
-  Rec rr[NE];
+  float4 rpos[NE];  // the staged records in registers: position, then {id, site}
+  int4 rids[NE];
   int cell[NE], rank[NE], gi[NE];
   // elements base + k·blockDim + tid: record, global index, flat cell index
   // (-1: not in the block + halo)
@@ -2556,26 +2573,31 @@ __device__ bool tile_load(const KParams& P, const Dev& d, const TileGeo& G, Tile
 #pragma unroll
     for (int k = 0; k < NE; ++k) {
       const int q = base + k * (int)blockDim.x + (int)threadIdx.x;
-      gi[k] = q < nseq ? tile_elem(d, T, G, q, ax[k], ay[k], kd[k]) : -1;
+      gi[k] = q < nseq ? tile_elem(P, d, T, G, q, ax[k], ay[k], kd[k]) : -1;
     }
 #pragma unroll
     for (int k = 0; k < NE; ++k)
-      if (gi[k] >= 0) rr[k] = d.rec[gi[k]];
+      if (gi[k] >= 0) {
+        const int4* rp = reinterpret_cast<const int4*>(d.rec + gi[k]);
+        const int4 a = rp[0], b = rp[1];
+        rpos[k] = make_float4(__int_as_float(a.x), __int_as_float(a.y), __int_as_float(a.z), __int_as_float(a.w));
+        rids[k] = b;
+      }
 #pragma unroll
     for (int k = 0; k < NE; ++k) {
-      const float xr = rr[k].pos.x;
+      const float xr = rpos[k].x;
       cell[k] = -1;
       if (gi[k] < 0) continue;
       int x = ax[k], y = ay[k];
       if (kd[k] >= 0) {  // home record: its cell from the code; outliers come from the list
-        const int c = rec_code(rr[k].id);
+        const int c = rec_code(make_int2(rids[k].x, rids[k].y));
         if (c == RID_OUT) continue;
         x += c % 3 - 1;
         y += c / 3 - 1;
       }
       const int hx = x - G.cx0, hy = y - G.cy0;
       if (hx < 0 || hx >= hw || hy < 0 || hy >= hh) continue;
-      const int kind = (rr[k].id.x & RID_LIG) ? 1 : 0, seg = hy * 2 + kind;
+      const int kind = (rids[k].x & RID_LIG) ? 1 : 0, seg = hy * 2 + kind;
       const int b = sub_bin(SC, hx, xr);
       cell[k] = (seg * (hw * SUBC + 1) + b) | (seg | hx << 8) << 16;  // flat bin | LDS tag << 16
     }
@@ -2602,9 +2624,9 @@ __device__ bool tile_load(const KParams& P, const Dev& d, const TileGeo& G, Tile
   if (n > P.tcap) return false;
   // LDS record: the home position in place of the slot (tile_global)
   auto place = [&](int k, int l) {
-    T.pos[l] = rr[k].pos;
-    T.id[l] = make_int2((gi[k] >> 1) | (rr[k].id.x & ~RID_PID), rr[k].id.y);
-    if (site) site[l] = rr[k].site;
+    T.pos[l] = rpos[k];
+    T.id[l] = make_int2((gi[k] >> 1) | (rids[k].x & ~RID_PID), rids[k].y);
+    if (site) site[l] = make_float2(__int_as_float(rids[k].z), __int_as_float(rids[k].w));
     T.tag[l] = (uint16_t)(cell[k] >> 16);
   };
   if (one) {
@@ -2667,16 +2689,25 @@ __device__ __forceinline__ void item_ranges(const KParams& P, const TileLds& T, 
 // six ranges (kind 0 rows, kind 1 rows) of a scanning record l, or false.
 // Every lane of a wave holds one record's ranges; the wave walks the
 // concatenation of its lanes' ranges 64 pairs at a time — lane L takes pair
-// j + L, finds its owner lane by a binary search over the lanes' inclusive
-// prefix and its neighbour record from the owner's packed range starts — so
-// every lane checks a pair, the owner's record is a broadcast LDS read and the
-// neighbour records of consecutive lanes are mostly consecutive.
+// j + L, finds its owner lane and its neighbour record from the owner's packed
+// range starts — so every lane checks a pair, the owner's record is a
+// broadcast LDS read and the neighbour records of consecutive lanes are mostly
+// consecutive.
+// Owner lookup (WALK_BITS): the lanes that have pairs are first moved to the
+// front in lane order (ds_permute), so every owner's range is non-empty and
+// their starts are distinct; each owner sets the bit of its first pair in a
+// per-wave bitmap in LDS, and the owner of pair q is (starts <= q) − 1: one
+// broadcast read of the chunk's 64 bits and a popcount per lane, in place of
+// a six-step binary search of dependent lane shuffles.
 // chk(l, r) for every pair; all threads call (no barrier).
 #ifndef WALK_STRIDE  // (A/B builds: 0 = each wave takes 64 consecutive records)
 #define WALK_STRIDE 1
 #endif
+#ifndef WALK_BITS  // (A/B builds: 0 = binary search over the lanes' prefix)
+#define WALK_BITS 1
+#endif
 template <class Rng, class Chk>
-__device__ __forceinline__ void tile_walk(const TileGeo& G, const TileLds& T, Rng rng, Chk chk) {
+__device__ __forceinline__ void tile_walk(const TileGeo& G, const TileLds& T, uint32_t* wbits, Rng rng, Chk chk) {
   const int n = T.n, lane = __lane_id();
   // records go to the waves round-robin (record base + lane·nw + wave): the
   // staged records are in bin order, so each wave samples the whole block and
@@ -2705,6 +2736,20 @@ __device__ __forceinline__ void tile_walk(const TileGeo& G, const TileLds& T, Rn
       pk[k] = (uint32_t)(item ? r0[k] : 0) | (uint32_t)tot << 16;
       tot += len;
     }
+#if WALK_BITS
+    const uint64_t Z = __ballot(tot > 0);
+    if (Z == 0) continue;  // (uniform)
+    {  // owners to the front: lane `dst` receives this lane's ranges and its lane index
+      const uint64_t lt = (1ull << lane) - 1ull;
+      const int nz = __popcll(Z);
+      const int da = (tot > 0 ? __popcll(Z & lt) : nz + __popcll(~Z & lt)) << 2;
+      tot = __builtin_amdgcn_ds_permute(da, tot | lane << 24);
+#pragma unroll
+      for (int k = 0; k < 6; ++k) pk[k] = (uint32_t)__builtin_amdgcn_ds_permute(da, (int)pk[k]);
+    }
+    const int olane = (int)((uint32_t)tot >> 24);
+    tot &= 0xffffff;
+#endif
     int inc = tot;  // wave-level inclusive prefix (every lane of the wave is here)
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -2715,6 +2760,40 @@ __device__ __forceinline__ void tile_walk(const TileGeo& G, const TileLds& T, Rn
 #if !WALK_STRIDE
     const int l0 = l - lane;
 #endif
+#if WALK_BITS
+    // excl < 6 TCAP · 64 < 2^24: one word carries the owner's first pair and lane
+    const int ew = excl | olane << 24;
+    uint32_t* wb = wbits + (threadIdx.x >> 6) * WALK_WIN;
+    const uint32_t le_lo = lane < 32 ? (2u << lane) - 1u : ~0u, le_hi = lane < 32 ? 0u : (2u << (lane - 32)) - 1u;
+    int before = 0;  // owners whose first pair precedes the chunk
+    for (int w0 = 0; w0 < wtot; w0 += 32 * WALK_WIN) {
+      // (a wave's LDS operations complete in order: the clear, the bits and
+      // the reads below need no barrier)
+      if (lane < WALK_WIN) wb[lane] = 0u;
+      if (tot > 0 && excl >= w0 && excl < w0 + 32 * WALK_WIN)
+        atomicOr(&wb[(excl - w0) >> 5], 1u << ((excl - w0) & 31));
+      const int wend = min(wtot, w0 + 32 * WALK_WIN);
+      for (int j = w0; j < wend; j += 64) {
+        const uint2 m = *reinterpret_cast<const uint2*>(wb + ((j - w0) >> 5));
+        const int o = before + __popc(m.x & le_lo) + __popc(m.y & le_hi) - 1;
+        before += __popc(m.x) + __popc(m.y);
+        const int q = j + lane, oa = o << 2;
+        const int eo = __builtin_amdgcn_ds_bpermute(oa, ew);
+        uint32_t sel = (uint32_t)__builtin_amdgcn_ds_bpermute(oa, (int)pk[0]);
+        const int t = q - (eo & 0xffffff);
+#pragma unroll
+        for (int k = 1; k < 6; ++k) {
+          const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute(oa, (int)pk[k]);
+          if ((int)(v >> 16) <= t) sel = v;
+        }
+#if WALK_STRIDE
+        if (q < wtot) chk(base + ((uint32_t)eo >> 24) * nw + wv, (int)(sel & 0xffffu) + t - (int)(sel >> 16));
+#else
+        if (q < wtot) chk(l0 + ((uint32_t)eo >> 24), (int)(sel & 0xffffu) + t - (int)(sel >> 16));
+#endif
+      }
+    }
+#else
     for (int j = 0; j < wtot; j += 64) {
       const int q = j + lane;
       int o = 0;  // owner: the number of lanes whose inclusive prefix is <= q
@@ -2735,6 +2814,7 @@ __device__ __forceinline__ void tile_walk(const TileGeo& G, const TileLds& T, Rn
       if (q < wtot) chk(l0 + o, (int)(sel & 0xffffu) + t - (int)(sel >> 16));
 #endif
     }
+#endif
   }
 }
 
@@ -2866,12 +2946,13 @@ __device__ __forceinline__ void col_exact_one(const KParams& P, const Dev& d, in
 }
 
 // Records of a dense block's staging sequence (the home records of its home
-// region, then the outlier list) from global memory: f(record index) for
-// elements start, start + stride, ...  A home record coded RID_OUT is
-// skipped (it is on the outlier list).
+// region, then its outlier bucket, or the whole outlier list when the bucket
+// overflowed: obkt < 0) from global memory: f(record index) for elements
+// start, start + stride, ...  A home record coded RID_OUT is skipped (it is an
+// outlier).
 template <class F>
-__device__ __forceinline__ void dense_records(const KParams& P, const Dev& d, const TileGeo& G, int start, int stride,
-                                              F f) {
+__device__ __forceinline__ void dense_records(const KParams& P, const Dev& d, const TileGeo& G, int obkt, int nout,
+                                              int start, int stride, F f) {
   const int xlo = max(G.hx0, 0), xhi = min(G.hx0 + G.mw - 1, P.ncx - 1);
   int q = 0;  // running element index
   for (int seg = 0; seg < G.nhseg; ++seg) {
@@ -2884,6 +2965,11 @@ __device__ __forceinline__ void dense_records(const KParams& P, const Dev& d, co
       if (rec_code(d.rec[ri].id) != RID_OUT) f(ri);
     }
     q += n;
+  }
+  if (obkt >= 0) {
+    for (int k = ((start - q) % stride + stride) % stride; k < nout; k += stride)
+      f(d.tout[(size_t)obkt * TOUT_CAP + k].x);
+    return;
   }
   const int no = (int)min(d.ctl->n_outl, d.outl_cap);
   for (int k = ((start - q) % stride + stride) % stride; k < no; k += stride) f(d.outl[k].x);
@@ -2908,8 +2994,9 @@ __device__ __noinline__
 __device__ __forceinline__
 #endif
 void dense_block(const KParams& P, const Dev& d, int4 blk, uint32_t tag) {
-  const TileGeo G = tile_geo(blk.x, blk.y, blk.z, blk.w);
-  dense_records(P, d, G, threadIdx.x, blockDim.x, [&](int ri) {
+  const TileGeo G = tile_geo(blk.x & 0xffff, blk.x >> 16, blk.y & 0xffff, blk.y >> 16);
+  const int obkt = blk.z, nout = blk.w;
+  dense_records(P, d, G, obkt, nout, threadIdx.x, blockDim.x, [&](int ri) {
     int x, y;
     rec_cell_exact(P, d, ri, x, y);
     if (x < G.x0 || x >= G.x0 + G.w || y < G.y0 || y >= G.y0 + G.h) return;
@@ -2922,7 +3009,7 @@ void dense_block(const KParams& P, const Dev& d, int4 blk, uint32_t tag) {
     }
     const bool rx = rxn_item(me);
     if (!prop && !rx) return;
-    dense_records(P, d, G, 0, 1, [&](int rn) {
+    dense_records(P, d, G, obkt, nout, 0, 1, [&](int rn) {
       int ox, oy;
       rec_cell_exact(P, d, rn, ox, oy);
       if (abs(ox - x) > 1 || abs(oy - y) > 1) return;
@@ -3115,7 +3202,7 @@ __device__ __forceinline__ bool pair_scan_block(const KParams& P, const Dev& d, 
   Bc.n = 0;
   Br.n = 0;
   tile_walk(
-      G, T,
+      G, T, T.u.l.wbits,
       [&](int l, int seg, int hx, int* r0, int* r1) {
         const int2 me = T.id[l];
         bool prop = me.x < 0;  // proposal record: collision candidates
@@ -3186,7 +3273,7 @@ __global__ void __launch_bounds__(256, PAIR_WAVES) k_pair_scan(KParams P, Dev d)
   Stamper S(0);
   if (!pair_scan_block(P, d, tile_geo(x0, y0, w, h), T, site, Lc, Lr, S) && threadIdx.x == 0) {
     const uint32_t o = atomicAdd(&d.ctl->n_dense, 1u);  // k_col_exact takes it
-    if (o < d.dense_cap) d.dense[o] = make_int4(x0, y0, w, h);
+    if (o < d.dense_cap) d.dense[o] = make_int4(x0 | y0 << 16, w | h << 16, T.obkt, (int)T.nout);
     else atomicOr(&d.ctl->err, ERR_EDGES);
   }
   if (P.dbg_stage == 1 || P.dbg_stage == 3) return;

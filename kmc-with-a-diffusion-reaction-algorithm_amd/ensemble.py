@@ -44,3 +44,43 @@ def reduce(obs: np.ndarray, device=None, group=None):
     tot_prot, tot_clu = s[:, 4].astype(np.float64), s[:, 5].astype(np.float64)
     cluster = np.divide(tot_prot, tot_clu, out=np.zeros_like(tot_prot), where=tot_clu != 0)
     return s, m, cluster
+
+
+class Reducer:
+    """reduce() with buffers allocated once: pinned host staging and device
+    tensors for K steps (the bench's timed window reduces without allocating).
+    Same result as reduce()."""
+
+    def __init__(self, k: int, device=None, group=None):
+        import torch
+
+        self.k, self.device, self.group = k, device, group
+        pin = device is not None and torch.cuda.is_available()
+        self.hs = torch.zeros((k, len(SUM_FIELDS)), dtype=torch.int64, pin_memory=pin)
+        self.hm = torch.zeros((k, len(MAX_FIELDS)), dtype=torch.int64, pin_memory=pin)
+        self.ds = self.hs.to(device) if device is not None else self.hs
+        self.dm = self.hm.to(device) if device is not None else self.hm
+
+    def reduce(self, obs: np.ndarray):
+        import torch
+        import torch.distributed as dist
+
+        if len(obs) != self.k:
+            return reduce(obs, device=self.device, group=self.group)
+        s, m = pack(obs)
+        self.hs.numpy()[...] = s
+        self.hm.numpy()[...] = m
+        if self.device is not None:
+            self.ds.copy_(self.hs, non_blocking=True)
+            self.dm.copy_(self.hm, non_blocking=True)
+        if dist.is_available() and dist.is_initialized():
+            dist.all_reduce(self.ds, op=dist.ReduceOp.SUM, group=self.group)
+            dist.all_reduce(self.dm, op=dist.ReduceOp.MAX, group=self.group)
+        if self.device is not None:
+            self.hs.copy_(self.ds, non_blocking=True)
+            self.hm.copy_(self.dm, non_blocking=True)
+            torch.cuda.current_stream(self.device).synchronize()
+        s, m = self.hs.numpy().copy(), self.hm.numpy().copy()
+        tot_prot, tot_clu = s[:, 4].astype(np.float64), s[:, 5].astype(np.float64)
+        cluster = np.divide(tot_prot, tot_clu, out=np.zeros_like(tot_prot), where=tot_clu != 0)
+        return s, m, cluster

@@ -32,6 +32,8 @@ def _worker(rank, world, port, out):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     obs = _replica_obs(rank)
     s, m, cluster = ensemble.reduce(obs)
+    s2, m2, c2 = ensemble.Reducer(len(obs)).reduce(obs)  # preallocated buffers (bench.py's timed window)
+    assert np.array_equal(s, s2) and np.array_equal(m, m2) and np.array_equal(cluster, c2)
     if rank == 0:
         np.savez(out, s=s, m=m, cluster=cluster)
     dist.destroy_process_group()

@@ -108,6 +108,67 @@ def test_global_tile_path_dense(monkeypatch, tcap):
     assert engine.state_hash(p, sim.get_state()) == o.hash()
 
 
+@pytest.mark.parametrize("tout_cap", [None, "0"])
+def test_global_tile_path_with_outliers(monkeypatch, capfd, tout_cap):
+    # every tile on the dense list (KMC_DEBUG_TCAP=0) and no re-sort: the
+    # brute force reads each tile's home records and its outlier bucket
+    # (dense_records) — or, when the bucket overflowed (capacity 0), the whole
+    # outlier list — with their own stride arithmetic and RID_OUT skip
+    import re
+
+    monkeypatch.setenv("KMC_DEBUG_TCAP", "0")
+    monkeypatch.setenv("KMC_RESORT", "0")
+    monkeypatch.setenv("KMC_DEBUG_COUNTS", "1")
+    if tout_cap is not None:
+        monkeypatch.setenv("KMC_DEBUG_TOUT_CAP", tout_cap)
+    p = params(seed=47, **DENSE)
+    o = O.Oracle(p)
+    o.init_placement()
+    sim = engine.Simulation(p)
+    sim.set_state(o.get_state())
+    obs = np.concatenate([sim.step(500) for _ in range(3)])
+    obs_o, _ = o.step(1500, want_hashes=False)
+    assert np.array_equal(obs, obs_o)
+    assert engine.state_hash(p, sim.get_state()) == o.hash()
+    outl = [int(x) for x in re.findall(r"outliers (\d+)", capfd.readouterr().err)]
+    assert outl and outl[-1] > 10, f"too few outlier records to reach the dense path's outlier loop: {outl}"
+
+
+def test_searched_home_lookup(monkeypatch):
+    # KMC_DEBUG_HTAG=0: no tile tags its home entries, so every staged home
+    # record finds its (segment, column) by the binary searches of tile_elem
+    # (the path of a tile with more than HTAG_MAX home entries)
+    monkeypatch.setenv("KMC_DEBUG_HTAG", "0")
+    p = params(seed=53, **DENSE)
+    o = O.Oracle(p)
+    o.init_placement()
+    sim = engine.Simulation(p)
+    sim.set_state(o.get_state())
+    obs = sim.step(1500)
+    obs_o, _ = o.step(1500, want_hashes=False)
+    assert np.array_equal(obs, obs_o)
+    assert engine.state_hash(p, sim.get_state()) == o.hash()
+
+
+def test_record_step_stamps(monkeypatch):
+    # KMC_DEBUG_RECS=1: every record is stamped with its step when written and
+    # k_rec_check raises ERR_RESOLVE (kmc_step fails) if any of the 2N records
+    # was not rewritten by the kernel that moved its protein this step —
+    # through free moves, complexes, lay-downs, alignments, rejections and
+    # re-sorts
+    monkeypatch.setenv("KMC_DEBUG_RECS", "1")
+    p = params(seed=59, **DENSE)
+    o = O.Oracle(p)
+    o.init_placement()
+    sim = engine.Simulation(p)
+    sim.set_state(o.get_state())
+    obs = sim.step(2000)
+    obs_o, _ = o.step(2000, want_hashes=False)
+    assert np.array_equal(obs, obs_o)
+    st = o.stats()
+    assert st["complex"] > 0 and st["laydown"] > 0 and st["reject"] > 0
+
+
 def test_frequent_slot_resort_dense(monkeypatch):
     # slots re-sorted every 7 steps while bonds form and break: bond fields,
     # random-stream keys and unit keys must survive the renumbering
@@ -237,6 +298,41 @@ def test_list_overflow_grow_and_replay(monkeypatch, capfd):
     import re
     replays = [int(x) for x in re.findall(r"replays (\d+)", capfd.readouterr().err)]
     assert replays and replays[-1] > 0, "the lists never overflowed: the replay path was not exercised"
+
+
+@pytest.mark.parametrize("span", [None, "0"])
+def test_list_overflow_replay_across_calls(monkeypatch, capfd, span):
+    # the snapshot is kept across kmc_step calls (KMC_SNAP_SPAN steps, default
+    # 4096): with lists 2^10 times too small and 60 short calls, an overflow in
+    # a later call restores the snapshot an earlier call took and replays the
+    # steps already returned before it runs the failing chunk again.  Span 0:
+    # a snapshot per chunk (the round-3 behaviour).  The trajectory must not
+    # change.
+    import re
+
+    monkeypatch.setenv("KMC_DEBUG_CAP_SHIFT", "10")
+    monkeypatch.setenv("KMC_DEBUG_COUNTS", "1")
+    if span is not None:
+        monkeypatch.setenv("KMC_SNAP_SPAN", span)
+    p = params(seed=37, **DENSE)
+    o = O.Oracle(p)
+    o.init_placement()
+    sim = engine.Simulation(p)
+    sim.set_state(o.get_state())
+    obs = np.concatenate([sim.step(25) for _ in range(60)])
+    obs_o, _ = o.step(1500, want_hashes=False)
+    assert np.array_equal(obs, obs_o)
+    assert engine.state_hash(p, sim.get_state()) == o.hash()
+    assert sim.current_step == 1500
+    rows = [tuple(int(x) for x in m) for m in
+            re.findall(r"kmc step (\d+):.*replays (\d+), snapshots (\d+)", capfd.readouterr().err)]
+    assert len(rows) == 60
+    if span is None:
+        assert rows[-1][2] == 1, "one snapshot for 1500 steps"
+        later = [r for k, r in enumerate(rows[1:], 1) if r[1] > rows[k - 1][1]]
+        assert later, "no overflow after the first call: the cross-call replay was not exercised"
+    else:
+        assert rows[-1][2] == 60
 
 
 @pytest.mark.parametrize("tout_cap", [None, "2", "0"])
