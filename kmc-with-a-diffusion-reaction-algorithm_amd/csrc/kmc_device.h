@@ -37,6 +37,7 @@ struct KParams {
                       // lowered only by KMC_DEBUG_CX_LIMIT to exercise the rebuild)
   int htag_max;   // tile home entries tagged for the direct lookup (<= HTAG_MAX; lowered only by KMC_DEBUG_HTAG)
   int dbg_recs;   // debug (KMC_DEBUG_RECS=1): every record stamped with its step and checked before the pair scan
+  int dbg_cand;   // diagnostics (KMC_DEBUG_CAND=1): candidate / reaction-pair outcome counts (Ctl::cand_kind)
 };
 
 // per-step control block in device memory (replayable without host writes)
@@ -67,6 +68,10 @@ struct Ctl {
                           // full, or a dirty list overflowed); only k_finalize writes it
   uint32_t n_forced;      // diagnostics: full complex rebuilds latched by force_full since the state was set
   uint32_t last_outl;     // diagnostics: the previous step's outlier records (n_outl)
+  uint32_t cand_kind[6];  // diagnostics (KMC_DEBUG_CAND) since the state was set: collision candidates
+                          // of kind pair A-A, A-B, B-B (proposal kind + other kind), tested / colliding
+  uint32_t rxn_kind[4];   // diagnostics (KMC_DEBUG_CAND): reaction pairs tested, final-final, within the
+                          // first distance gate, accepting
   uint64_t vtag;          // BFS tag counter for the overflow path
   uint64_t stamps[24];    // diagnostic build (-DKMC_STAMPS) only: phase cycles (tile scans, complexes)
 };
@@ -95,15 +100,35 @@ enum : uint32_t { S_ACC = 1, S_PEND = 2, S_REJ = 3 };  // unit fate this step (a
 // SoA `[(bead·3 + c)][n]`; k_gather_beads converts at the boundary.
 #define ROWS_A 24
 #define ROWS_B 12
+// BEAD_BLOCK 1: the rows are blocked by 64 slots instead — element (r, i) is
+// number ((i / 64)·rows + r)·64 + i mod 64, so the rows of one wave's 64
+// slots form one contiguous run (rows × 1 KiB) rather than `rows` streams n
+// elements apart; the buffers then hold a whole number of 64-slot blocks.
+#ifndef BEAD_BLOCK
+#define BEAD_BLOCK 0
+#endif
+__host__ __device__ __forceinline__ size_t bead_elem(int i, int r, int n, int rows) {
+#if BEAD_BLOCK
+  (void)n;
+  return ((size_t)(i >> 6) * rows + r) * 64 + (i & 63);
+#else
+  (void)rows;
+  return (size_t)r * n + i;
+#endif
+}
+// slots a bead buffer of n proteins holds
+__host__ __device__ __forceinline__ size_t bead_slots(int n) {
+  return BEAD_BLOCK ? ((size_t)n + 63) / 64 * 64 : (size_t)n;
+}
 __host__ __device__ __forceinline__ size_t bead_off_a(int i, int j, int k, int c, int NA) {
   const int row = c < 2 ? (j - 1) * 4 + (k - 1) : 16 + ((j - 1) >> 1) * 4 + (k - 1);
   const int half = c < 2 ? c : ((j - 1) & 1);
-  return ((size_t)row * NA + i) * 2 + half;
+  return bead_elem(i, row, NA, ROWS_A) * 2 + half;
 }
 __host__ __device__ __forceinline__ size_t bead_off_b(int i, int j, int k, int c, int NB) {
   const int row = c < 2 ? (j - 1) * 2 + (k - 1) : 8 + ((j - 1) >> 1) * 2 + (k - 1);
   const int half = c < 2 ? c : ((j - 1) & 1);
-  return ((size_t)row * NB + i) * 2 + half;
+  return bead_elem(i, row, NB, ROWS_B) * 2 + half;
 }
 struct Beads {
   double* a;
@@ -113,10 +138,10 @@ struct Beads {
   __device__ __forceinline__ double& B(int i, int j, int k, int c) const { return b[bead_off_b(i, j, k, c, NB)]; }
   // whole double2 rows (one 16-byte access)
   __device__ __forceinline__ double2& A2(int i, int row) const {
-    return reinterpret_cast<double2*>(a)[(size_t)row * NA + i];
+    return reinterpret_cast<double2*>(a)[bead_elem(i, row, NA, ROWS_A)];
   }
   __device__ __forceinline__ double2& B2(int i, int row) const {
-    return reinterpret_cast<double2*>(b)[(size_t)row * NB + i];
+    return reinterpret_cast<double2*>(b)[bead_elem(i, row, NB, ROWS_B)];
   }
   // (x, y) of a bead in one access
   __device__ __forceinline__ double2 Axy(int i, int j, int k) const { return A2(i, (j - 1) * 4 + (k - 1)); }

@@ -299,10 +299,10 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   d.cur.NA = d.nxt.NA = NA;
   d.cur.NB = d.nxt.NB = NB;
   int rc = KMC_OK;
-  rc |= dalloc(s, &d.cur.a, (size_t)48 * NA);
-  rc |= dalloc(s, &d.nxt.a, (size_t)48 * NA);
-  rc |= dalloc(s, &d.cur.b, (size_t)24 * NB);
-  rc |= dalloc(s, &d.nxt.b, (size_t)24 * NB);
+  rc |= dalloc(s, &d.cur.a, 48 * bead_slots(NA));
+  rc |= dalloc(s, &d.nxt.a, 48 * bead_slots(NA));
+  rc |= dalloc(s, &d.cur.b, 24 * bead_slots(NB));
+  rc |= dalloc(s, &d.nxt.b, 24 * bead_slots(NB));
   rc |= dalloc(s, &d.a_int, (size_t)5 * NA);
   rc |= dalloc(s, &d.b_int, (size_t)8 * NB);
   rc |= dalloc(s, &d.owner, N);
@@ -383,7 +383,7 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
     const double rho = (double)N * K.cs * K.cs / std::max(1.0, p->box_x * p->box_y);  // proteins per cell
     int t = TILE_MAX;
     // (a tile whose records still overflow TCAP goes onto the dense list and
-    // is brute-forced from global memory by k_col_exact: the mean is kept at
+    // is brute-forced from global memory by k_col_dense: the mean is kept at
     // 0.75 TCAP, > 7 Poisson sigmas below TCAP at the benchmark densities)
     while (t > 4 && (t * t * rho > 205.0 || (t + 2) * (t + 2) * 2.0 * rho > 0.75 * TCAP)) --t;
     const char* te = getenv("KMC_TILE");
@@ -400,6 +400,8 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
     const char* ht = getenv("KMC_DEBUG_HTAG");  // debug: fewer tagged home entries (the searched lookup)
     K.htag_max = HTAG_MAX;
     if (ht && *ht) K.htag_max = std::max(0, std::min(HTAG_MAX, atoi(ht)));
+    const char* dca = getenv("KMC_DEBUG_CAND");
+    K.dbg_cand = dca && *dca == '1';
     const char* dr = getenv("KMC_DEBUG_RECS");
     K.dbg_recs = dr && *dr == '1';
     if (K.dbg_recs && dalloc(s, &d.rec_step, 2 * (size_t)N) != KMC_OK) {
@@ -569,8 +571,8 @@ static int snapshot(kmc_sim* s, bool restore) {
   hipStream_t st = s->stream;
   if (!s->snap_ctl) {
     int rc = KMC_OK;
-    rc |= dalloc(s, &s->snap_a, 48 * NA);
-    rc |= dalloc(s, &s->snap_b, 24 * NB);
+    rc |= dalloc(s, &s->snap_a, 48 * bead_slots((int)NA));
+    rc |= dalloc(s, &s->snap_b, 24 * bead_slots((int)NB));
     rc |= dalloc(s, &s->snap_ai, 5 * NA);
     rc |= dalloc(s, &s->snap_bi, 8 * NB);
     rc |= dalloc(s, &s->snap_id, N);
@@ -582,8 +584,8 @@ static int snapshot(kmc_sim* s, bool restore) {
     return restore ? hipMemcpyAsync(live, snap, bytes, hipMemcpyDeviceToDevice, st)
                    : hipMemcpyAsync(snap, live, bytes, hipMemcpyDeviceToDevice, st);
   };
-  HIPCHK(s, cp(d.cur.a, s->snap_a, sizeof(double) * 48 * NA));
-  HIPCHK(s, cp(d.cur.b, s->snap_b, sizeof(double) * 24 * NB));
+  HIPCHK(s, cp(d.cur.a, s->snap_a, sizeof(double) * 48 * bead_slots((int)NA)));
+  HIPCHK(s, cp(d.cur.b, s->snap_b, sizeof(double) * 24 * bead_slots((int)NB)));
   HIPCHK(s, cp(d.a_int, s->snap_ai, sizeof(int32_t) * 5 * NA));
   HIPCHK(s, cp(d.b_int, s->snap_bi, sizeof(int32_t) * 8 * NB));
   HIPCHK(s, cp(d.id_of, s->snap_id, sizeof(int32_t) * N));
@@ -787,8 +789,8 @@ static int launch_step(kmc_sim* s, bool re_sort) {
   }
   if (s->poison) {
     // debug: every bead of R_new must be rewritten by a proposal or a revert
-    (void)hipMemsetAsync(d.nxt.a, 0xff, sizeof(double) * 48 * (size_t)K.NA, st);
-    (void)hipMemsetAsync(d.nxt.b, 0xff, sizeof(double) * 24 * (size_t)K.NB, st);
+    (void)hipMemsetAsync(d.nxt.a, 0xff, sizeof(double) * 48 * bead_slots(K.NA), st);
+    (void)hipMemsetAsync(d.nxt.b, 0xff, sizeof(double) * 24 * bead_slots(K.NB), st);
   }
   if (K.NB > 0) {
     const int full = (s->need_full || re_sort || s->always_full) ? 1 : 0;
@@ -824,8 +826,14 @@ static int launch_step(kmc_sim* s, bool re_sort) {
   const int ntiles = s->ntiles;
   // collision candidates and reaction candidates, one staging of each tile
   TIMED(KI_PAIR_SCAN, (k_pair_scan<<<ntiles, 256, 0, st>>>(K, d)));
-  // (at least 64 workgroups: k_col_exact also scans the dense blocks, one per workgroup)
-  TIMED(KI_COL_EXACT, (k_col_exact<<<std::max(gX, 64), T, 0, st>>>(K, d)));
+  // the tiles too dense for the pair scan's LDS, one per workgroup, then the
+  // exact tests of the candidates
+  TIMED(KI_COL_EXACT, {
+#if DENSE_KERNEL
+    k_col_dense<<<64, T, 0, st>>>(K, d);
+#endif
+    k_col_exact<<<std::max(gX, 64), T, 0, st>>>(K, d);
+  });
   TIMED(KI_COL_ROUNDS, {
     k_col_round<<<gX, T, 0, st>>>(K, d, 0);
     k_col_units<<<gX, T, 0, st>>>(K, d, 0);
@@ -1007,7 +1015,20 @@ int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out) {
       fprintf(stderr, "kmc step %lld: candidates %u conflicts %u pending-units %u rejected %u rxn-pairs %u rl-edges %u cis-edges %u bfs-overflow %u outliers %u (list growth 2^%d, replays %lld, snapshots %lld, forced rebuilds %u)\n",
               (long long)s->step_done, l[0], l[1], l[2], l[3], l[4], l[5], l[6], l[7], s->ctl_host->last_outl, s->grow,
               (long long)s->n_replays, (long long)s->n_snapshots, s->ctl_host->n_forced);
+      if (s->K.dbg_cand) {
+        const uint32_t* c = s->ctl_host->cand_kind;
+        const uint32_t* r = s->ctl_host->rxn_kind;
+        fprintf(stderr, "kmc cand AA %u/%u AB %u/%u BB %u/%u (tested/colliding) rxn %u final %u gate %u accept %u\n",
+                c[0], c[1], c[2], c[3], c[4], c[5], r[0], r[1], r[2], r[3]);
+      }
       const uint64_t* t = s->ctl_host->stamps;
+#ifdef WALK_STATS
+      fprintf(stderr, "kmc walk AA %llu %llu %llu AB %llu %llu %llu BA %llu %llu %llu BB %llu %llu %llu "
+              "(walked, within xy reach, passing; cumulative)\n",
+              (unsigned long long)t[0], (unsigned long long)t[4], (unsigned long long)t[8], (unsigned long long)t[1],
+              (unsigned long long)t[5], (unsigned long long)t[9], (unsigned long long)t[2], (unsigned long long)t[6],
+              (unsigned long long)t[10], (unsigned long long)t[3], (unsigned long long)t[7], (unsigned long long)t[11]);
+#endif
       if (t[16])
         fprintf(stderr, "kmc stamps cx stage %llu rigid %llu checks %llu writeback %llu count %llu next %llu\n",
                 (unsigned long long)t[16], (unsigned long long)t[17], (unsigned long long)t[18],

@@ -1871,7 +1871,7 @@ __device__ __forceinline__ void move_member(const KParams& P, const Dev& d, int 
   double2* dst = reinterpret_cast<double2*>(IS_A ? d.nxt.a : d.nxt.b);
   double2 r[ROWS];
 #pragma unroll
-  for (int w = 0; w < ROWS; ++w) r[w] = ld_r(src[(size_t)w * n + i]);
+  for (int w = 0; w < ROWS; ++w) r[w] = ld_r(src[bead_elem(i, w, n, ROWS)]);
   const double dx = cp[0], dy = cp[1], PBx = cp[2], PBy = cp[3], cmx = cp[4], cmy = cp[5], cmz = cp[6];
   Rot t;
 #pragma unroll
@@ -1907,7 +1907,7 @@ __device__ __forceinline__ void move_member(const KParams& P, const Dev& d, int 
       r[rzr] = make_double2(rz(t, ox1, oy1, z1, cmx, cmy, cmz), rz(t, ox2, oy2, z2, cmx, cmy, cmz));
     }
 #pragma unroll
-  for (int w = 0; w < ROWS; ++w) st_n(dst[(size_t)w * n + i], r[w]);
+  for (int w = 0; w < ROWS; ++w) st_n(dst[bead_elem(i, w, n, ROWS)], r[w]);
   recs(1);
 }
 
@@ -2313,10 +2313,19 @@ __device__ __forceinline__ void wg_flush2(WgList& L0, const SList& o0, WgList& L
 // TCAP goes onto the dense list: k_col_exact brute-forces it from global
 // memory (its home records and its outlier bucket, dense_block).
 #ifndef TILE_MAX  // (overridable for tile-size sweeps: tools/build_variants.py)
-#define TILE_MAX 14
+#define TILE_MAX 13
 #endif
 #define HALO_MAX (TILE_MAX + 2)
-#define NSEG_MAX (2 * HALO_MAX)
+// Staged records are binned by (halo row, kind, column, half column).
+// (Measured and rejected, round 4: ligands split further by z — those above
+// every receptor's reach in a part of their own, with a second copy of the
+// ligands near the split for the ligand-ligand reach: 39 % fewer pairs walked
+// at C3, but the second copies and the larger bin table cost the staging 14 %
+// and the tile size at C5 (whose ligands sit at the membrane, most of them in
+// the overlap) — net +-4 % on the scan and a dense-path cliff when the tile
+// choice misjudges the copies.)
+#define NPART 2
+#define NSEG_MAX (NPART * HALO_MAX)
 #define HOME_MAX (TILE_MAX + 4)
 #define HSEG_MAX (2 * HOME_MAX)
 #ifndef SUBC  // sub-columns per cell in the LDS bins (x extent of the cut stencils: 130 / SUBC Å steps)
@@ -2488,7 +2497,7 @@ __device__ __forceinline__ int tile_elem(const KParams& P, const Dev& d, const T
 // for the brute-force path).
 __device__ bool tile_load(const KParams& P, const Dev& d, const TileGeo& G, TileLds& T, float2* site, Stamper& S) {
   const int hw = G.hw, hh = G.hh, mw = G.mw, nhseg = G.nhseg;
-  const int nflat = 2 * hh * (hw * SUBC + 1) + 1;
+  const int nflat = NPART * hh * (hw * SUBC + 1) + 1;
   const SubCol SC = sub_cols(P, G);
   __shared__ int wtot[16];
 #ifndef HDR_WAVE
@@ -2565,10 +2574,10 @@ __device__ bool tile_load(const KParams& P, const Dev& d, const TileGeo& G, Tile
   const bool one = nseq <= NE * (int)blockDim.x;  // every element held in registers through the binning
   float4 rpos[NE];  // the staged records in registers: position, then {id, site}
   int4 rids[NE];
-  int cell[NE], rank[NE], gi[NE];
+  int cell[NE], rank[NE], gi[NE], pre[NE];  // pre: sub-bin | column << 8 | halo row << 16, or -1
   // elements base + k·blockDim + tid: record, global index, flat cell index
   // (-1: not in the block + halo)
-  auto fetch = [&](int base) {
+  auto load = [&](int base) {
     int ax[NE], ay[NE], kd[NE];
 #pragma unroll
     for (int k = 0; k < NE; ++k) {
@@ -2585,8 +2594,7 @@ __device__ bool tile_load(const KParams& P, const Dev& d, const TileGeo& G, Tile
       }
 #pragma unroll
     for (int k = 0; k < NE; ++k) {
-      const float xr = rpos[k].x;
-      cell[k] = -1;
+      pre[k] = -1;
       if (gi[k] < 0) continue;
       int x = ax[k], y = ay[k];
       if (kd[k] >= 0) {  // home record: its cell from the code; outliers come from the list
@@ -2597,8 +2605,16 @@ __device__ bool tile_load(const KParams& P, const Dev& d, const TileGeo& G, Tile
       }
       const int hx = x - G.cx0, hy = y - G.cy0;
       if (hx < 0 || hx >= hw || hy < 0 || hy >= hh) continue;
-      const int kind = (rids[k].x & RID_LIG) ? 1 : 0, seg = hy * 2 + kind;
-      const int b = sub_bin(SC, hx, xr);
+      pre[k] = sub_bin(SC, hx, rpos[k].x) | hx << 8 | hy << 16;
+    }
+  };
+  auto bin = [&]() {
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+      cell[k] = -1;
+      if (pre[k] < 0) continue;
+      const int b = pre[k] & 0xff, hx = (pre[k] >> 8) & 0xff, hy = pre[k] >> 16;
+      const int seg = hy * NPART + ((rids[k].x & RID_LIG) ? 1 : 0);
       cell[k] = (seg * (hw * SUBC + 1) + b) | (seg | hx << 8) << 16;  // flat bin | LDS tag << 16
     }
   };
@@ -2608,11 +2624,13 @@ __device__ bool tile_load(const KParams& P, const Dev& d, const TileGeo& G, Tile
       if (cell[k] >= 0) rank[k] = atomicAdd(&T.cstart[cell[k] & 0xffff], 1);
   };
   if (one) {
-    fetch(0);
+    load(0);
+    bin();
     count();
   } else {
     for (int base = 0; base < nseq; base += NE * blockDim.x) {
-      fetch(base);
+      load(base);
+      bin();
       count();
     }
   }
@@ -2623,24 +2641,25 @@ __device__ bool tile_load(const KParams& P, const Dev& d, const TileGeo& G, Tile
   S(d, 3);
   if (n > P.tcap) return false;
   // LDS record: the home position in place of the slot (tile_global)
-  auto place = [&](int k, int l) {
+  auto place = [&](int k, int l, int cl) {
     T.pos[l] = rpos[k];
     T.id[l] = make_int2((gi[k] >> 1) | (rids[k].x & ~RID_PID), rids[k].y);
     if (site) site[l] = make_float2(__int_as_float(rids[k].z), __int_as_float(rids[k].w));
-    T.tag[l] = (uint16_t)(cell[k] >> 16);
+    T.tag[l] = (uint16_t)(cl >> 16);
   };
   if (one) {
 #pragma unroll
     for (int k = 0; k < NE; ++k)
-      if (cell[k] >= 0) place(k, T.cstart[cell[k] & 0xffff] + rank[k]);
+      if (cell[k] >= 0) place(k, T.cstart[cell[k] & 0xffff] + rank[k], cell[k]);
   } else {
     // a second pass with the counters as cursors: each ends at its cell's
     // end (= the next cell's start), shifted back afterwards
     for (int base = 0; base < nseq; base += NE * blockDim.x) {
-      fetch(base);
+      load(base);
+      bin();
 #pragma unroll
       for (int k = 0; k < NE; ++k)
-        if (cell[k] >= 0) place(k, atomicAdd(&T.cstart[cell[k] & 0xffff], 1));
+        if (cell[k] >= 0) place(k, atomicAdd(&T.cstart[cell[k] & 0xffff], 1), cell[k]);
     }
     __syncthreads();
     int v[SCAN_PER];
@@ -2661,24 +2680,25 @@ __device__ bool tile_load(const KParams& P, const Dev& d, const TileGeo& G, Tile
   return true;
 }
 
-// Record ranges of the neighbour kind `kind` around the record at (seg, hx),
-// float position (px, py), cut to the cells within `reach` of it: three row
-// ranges (empty when the row is out of reach).
+// Record ranges of the staged kind `part` for the record at (seg, hx): the
+// bins that can hold a record with x in [xlo, xhi] and y in [ylo, yhi] (an
+// interval around the record, less than a cell beyond its cell on each side):
+// three row ranges (empty when the row is out of reach).
 __device__ __forceinline__ void item_ranges(const KParams& P, const TileLds& T, const TileGeo& G, int seg, int hx,
-                                           float px, float py, int kind, float reach, int* r0, int* r1) {
-  const int hy = seg >> 1;
+                                           float xlo, float xhi, float ylo, float yhi, int part, int* r0, int* r1) {
+  const int hy = seg / NPART;
   const int cx = G.cx0 + hx, cy = G.cy0 + hy;
   const float xb = (float)(P.gx0 + cx * P.cs), yb = (float)(P.gy0 + cy * P.cs), cs = (float)P.cs;
-  const int lo = hx - (px - xb < reach ? 1 : 0), hi = hx + (xb + cs - px < reach ? 1 : 0);
-  // bins from the sub-column of px − reach in the first cell to that of
-  // px + reach in the last (sub_col is monotone: every record within reach
-  // of px in x lies in between)
+  const int lo = hx - (xlo < xb ? 1 : 0), hi = hx + (xhi > xb + cs ? 1 : 0);
+  // bins from the sub-column of xlo in the first cell to that of xhi in the
+  // last (sub_col is monotone: every record with x in the interval lies in
+  // between)
   const SubCol SC = sub_cols(P, G);
-  const int blo = sub_bin(SC, lo, px - reach), bhi = sub_bin(SC, hi, px + reach);
-  const bool down = py - yb < reach, up = yb + cs - py < reach;
+  const int blo = sub_bin(SC, lo, xlo), bhi = sub_bin(SC, hi, xhi);
+  const bool down = ylo < yb, up = yhi > yb + cs;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    const int s = (hy - 1 + k) * 2 + kind;
+    const int s = (hy - 1 + k) * NPART + part;
     const bool on = k == 1 || (k == 0 ? down : up);
     r0[k] = on ? tcs(T, G.hw, s, blo) : 0;
     r1[k] = on ? tcs(T, G.hw, s, bhi + 1) : 0;
@@ -2724,7 +2744,7 @@ __device__ __forceinline__ void tile_walk(const TileGeo& G, const TileLds& T, ui
     int r0[6], r1[6];
     bool item = false;
     if (l < n) {
-      const int tg = T.tag[l], seg = tg & 0xff, hx = tg >> 8, hy = seg >> 1;
+      const int tg = T.tag[l], seg = tg & 0xff, hx = tg >> 8, hy = seg / NPART;
       if (hy >= 1 && hy <= G.h && hx >= 1 && hx <= G.w) item = rng(l, seg, hx, r0, r1);
     }
     // range starts | pairs before the range << 16 (LDS indices < TCAP, counts < 6 TCAP)
@@ -2833,6 +2853,15 @@ __device__ __forceinline__ void pair_push(PairBuf& b, int2 v) {
   b.v3 = b.n == 3 ? x : b.v3;
   ++b.n;
 }
+// the same for the lanes where `on` holds, without a branch (selects only;
+// CHK_PRED A/B builds)
+__device__ __forceinline__ void pair_push_if(PairBuf& b, bool on, uint32_t x) {
+  b.v0 = on & (b.n == 0) ? x : b.v0;
+  b.v1 = on & (b.n == 1) ? x : b.v1;
+  b.v2 = on & (b.n == 2) ? x : b.v2;
+  b.v3 = on & (b.n == 3) ? x : b.v3;
+  b.n += on ? 1 : 0;
+}
 // active lanes of a wave; entries mapped through f on the way out
 template <class F>
 __device__ __forceinline__ void pair_flush(const PairBuf& b, WgList& L, const SList& out, uint32_t* err, F f) {
@@ -2869,6 +2898,15 @@ __device__ __forceinline__ void pair_flush(const PairBuf& b, WgList& L, const SL
 #define REACH_BB 131.0f
 #define REACH_RL 106.0f
 #define REACH_CIS 58.0f
+// cis search around the item's [3][3] site: the 16 Å site prefilter + 20.3 Å
+// from a receptor's site to its record point + 1.2 Å for float rounding
+#define REACH_CSITE 37.5f
+#ifndef CIS_SITE  // (A/B builds: 0 = the cis search around the record point, REACH_CIS)
+#define CIS_SITE 1
+#endif
+#ifndef CHK_PRED
+#define CHK_PRED 0
+#endif
 
 // ---------------------------------------------------------------- 4a. scan
 // Pass A: every proposal record (member m of unit u = its owner) is checked
@@ -2895,7 +2933,7 @@ __device__ __forceinline__ bool col_pair(int2 me, float4 mp, int2 id, float4 rp)
 
 // the receptor of record `me` can take part in a reaction (either bond free)
 __device__ __forceinline__ bool rxn_item(int2 me) {
-  return !(me.x & RID_LIG) && !((me.x & RID_ST2) && (me.x & RID_ST3));
+  return !(me.x & RID_LIG) & ((me.x & (RID_ST2 | RID_ST3)) != (RID_ST2 | RID_ST3));
 }
 
 // prefilter of one (receptor record, record) pair, finality aside
@@ -2931,7 +2969,13 @@ __device__ __forceinline__ void col_exact_one(const KParams& P, const Dev& d, in
   bool isnew = b.x < 0;
   Own o;
   load_own(P, d.nxt, m, o);
-  if (!exact_collide(P, o, isnew ? d.nxt : d.cur, q)) return;
+  const bool hit = exact_collide(P, o, isnew ? d.nxt : d.cur, q);
+  if (P.dbg_cand) {
+    const int kk = (m >= P.NA ? 1 : 0) + (q >= P.NA ? 1 : 0);
+    atomicAdd(&d.ctl->cand_kind[2 * kk], 1u);
+    if (hit) atomicAdd(&d.ctl->cand_kind[2 * kk + 1], 1u);
+  }
+  if (!hit) return;
   if (kq >= u) {
     mark_rej(d, u, tag);
     return;
@@ -3023,11 +3067,26 @@ void dense_block(const KParams& P, const Dev& d, int4 blk, uint32_t tag) {
   });
 }
 
+// The dense tiles in a kernel of their own (DENSE_KERNEL): the brute force's
+// registers would otherwise set k_col_exact's occupancy (107 against 58
+// VGPRs); it exits at once when no tile overflowed (every step at the
+// benchmark densities).
+#ifndef DENSE_KERNEL
+#define DENSE_KERNEL 1
+#endif
+__global__ void k_col_dense(KParams P, Dev d) {
+  const uint32_t tag = (d.ctl->step & 0x3fffffffu) << 2;
+  const uint32_t nd = min(d.ctl->n_dense, d.dense_cap);
+  for (uint32_t b = blockIdx.x; b < nd; b += gridDim.x) dense_block(P, d, d.dense[b], tag);
+}
+
 __global__ void k_col_exact(KParams P, Dev d) {
   const uint32_t tag = (d.ctl->step & 0x3fffffffu) << 2;
   __shared__ uint32_t pre[NSHARD + 1];
+#if !DENSE_KERNEL
   const uint32_t nd = min(d.ctl->n_dense, d.dense_cap);
   for (uint32_t b = blockIdx.x; b < nd; b += gridDim.x) dense_block(P, d, d.dense[b], tag);
+#endif
   const uint32_t n = sl_prefix(d.cand, pre);
   for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
     const int2 c = sl_at(d.cand, pre, t);
@@ -3133,18 +3192,25 @@ __device__ __forceinline__ void rej_copy(const KParams& P, const Dev& d, int m, 
   if (row >= (a ? ROWS_A : ROWS_B)) return;
   const double2* src = reinterpret_cast<const double2*>(a ? d.cur.a : d.cur.b);
   double2* dst = reinterpret_cast<double2*>(a ? d.nxt.a : d.nxt.b);
-  dst[(size_t)row * n + i] = src[(size_t)row * n + i];
+  const size_t e = bead_elem(i, row, n, a ? ROWS_A : ROWS_B);
+  dst[e] = src[e];
 }
 
-// One wave per rejected unit; its lanes take the (member, bead row) copies of
-// all members at once, so a complex costs the same few dependent loads as a
-// single protein.
+// One group of REJ_LANES lanes per rejected unit (four units per wave); its
+// lanes take the (member, bead row) copies of all members at once, so a
+// complex costs the same few dependent loads as a single protein, and a wave
+// carries four units' dependent chains at once (most rejected units are
+// single proteins of 12 or 24 rows).
+#ifndef REJ_LANES
+#define REJ_LANES 16
+#endif
 __global__ void k_rej_commit(KParams P, Dev d) {
   const int NA = P.NA;
   __shared__ uint32_t pre[NSHARD + 1];
   const uint32_t n = sl_prefix(d.rej, pre);
-  const int lane = threadIdx.x & 63;
-  const uint32_t w0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+  const int lane = threadIdx.x % REJ_LANES;
+  const uint32_t w0 = (blockIdx.x * blockDim.x + threadIdx.x) / REJ_LANES,
+                 nw = (gridDim.x * blockDim.x) / REJ_LANES;
   for (uint32_t t = w0; t < n; t += nw) {
     const int sl = d.slot_of[sl_at(d.rej, pre, t).x];
     const uint8_t kind = d.ukind[sl];
@@ -3157,7 +3223,7 @@ __global__ void k_rej_commit(KParams P, Dev d) {
       q = A_NEI3(d, sl) - 1;
     }
     auto member = [&](int k) { return kind == U_COMPLEX ? d.members[off + k] : (k ? q : sl); };
-    for (int e = lane; e < nm * ROWS_A; e += 64) rej_copy(P, d, member(e / ROWS_A), e % ROWS_A);
+    for (int e = lane; e < nm * ROWS_A; e += REJ_LANES) rej_copy(P, d, member(e / ROWS_A), e % ROWS_A);
   }
 }
 
@@ -3201,6 +3267,7 @@ __device__ __forceinline__ bool pair_scan_block(const KParams& P, const Dev& d, 
   PairBuf Bc, Br;
   Bc.n = 0;
   Br.n = 0;
+  bool bad = false;  // a collision candidate whose record has no owner key
   tile_walk(
       G, T, T.u.l.wbits,
       [&](int l, int seg, int hx, int* r0, int* r1) {
@@ -3213,14 +3280,33 @@ __device__ __forceinline__ bool pair_scan_block(const KParams& P, const Dev& d, 
         const bool rx = rxn_item(me);
         if (!prop && !rx) return false;
         const bool mA = !(me.x & RID_LIG);
-        float reach0 = prop ? (mA ? REACH_AA : REACH_AB) : 0.0f;
-        float reach1 = prop ? (mA ? REACH_AB : REACH_BB) : 0.0f;
-        if (rx && !(me.x & RID_ST3)) reach0 = fmaxf(reach0, REACH_CIS);
-        if (rx && !(me.x & RID_ST2) && NB > 0) reach1 = fmaxf(reach1, REACH_RL);
         const float4 mp = T.pos[l];
-        item_ranges(P, T, G, seg, hx, mp.x, mp.y, 0, reach0, r0, r1);
-        item_ranges(P, T, G, seg, hx, mp.x, mp.y, 1, reach1, r0 + 3, r1 + 3);
-        if (reach0 == 0.0f)
+        // kind 0: the collision reach around the record, and for the cis
+        // search a square around its [3][3] site (any cis partner has its
+        // site within 16 Å of this one, its record within 20.3 Å of its site)
+        const float rc0 = prop ? (mA ? REACH_AA : REACH_AB) : 0.0f;
+        float x0lo = mp.x - rc0, x0hi = mp.x + rc0, y0lo = mp.y - rc0, y0hi = mp.y + rc0;
+        const bool cis = rx && !(me.x & RID_ST3);
+        if (cis) {
+#if CIS_SITE
+          const float2 ms = site[l];
+          const float sxl = ms.x - REACH_CSITE, sxh = ms.x + REACH_CSITE, syl = ms.y - REACH_CSITE,
+                      syh = ms.y + REACH_CSITE;
+#else
+          const float sxl = mp.x - REACH_CIS, sxh = mp.x + REACH_CIS, syl = mp.y - REACH_CIS,
+                      syh = mp.y + REACH_CIS;
+#endif
+          x0lo = rc0 > 0.0f ? fminf(x0lo, sxl) : sxl;
+          x0hi = rc0 > 0.0f ? fmaxf(x0hi, sxh) : sxh;
+          y0lo = rc0 > 0.0f ? fminf(y0lo, syl) : syl;
+          y0hi = rc0 > 0.0f ? fmaxf(y0hi, syh) : syh;
+        }
+        float reach1 = prop ? (mA ? REACH_AB : REACH_BB) : 0.0f;
+        if (rx && !(me.x & RID_ST2) && NB > 0) reach1 = fmaxf(reach1, REACH_RL);
+        item_ranges(P, T, G, seg, hx, x0lo, x0hi, y0lo, y0hi, 0, r0, r1);
+        item_ranges(P, T, G, seg, hx, mp.x - reach1, mp.x + reach1, mp.y - reach1, mp.y + reach1, 1, r0 + 3,
+                    r1 + 3);
+        if (rc0 == 0.0f && !cis)
           for (int k = 0; k < 3; ++k) r1[k] = r0[k];
         if (reach1 == 0.0f)
           for (int k = 3; k < 6; ++k) r1[k] = r0[k];
@@ -3229,16 +3315,52 @@ __device__ __forceinline__ bool pair_scan_block(const KParams& P, const Dev& d, 
       [&](int il, int nl) {
         const int2 me = T.id[il], id = T.id[nl];
         const float4 mp = T.pos[il], rp = T.pos[nl];
-        if (me.x < 0 && me.y >= 0 && col_pair(me, mp, id, rp)) {
-          if (id.y < 0) atomicOr(&d.ctl->err, ERR_RESOLVE);
+#if CHK_PRED  // (A/B builds: predicates without branches, pushes by selects)
+        const bool colp = (me.x < 0) & (me.y >= 0) & col_pair(me, mp, id, rp);
+        const bool rxp = rxn_item(me) & rxn_pair(me, mp, site[il], id, rp, site[nl]);
+#else
+        const bool colp = me.x < 0 && me.y >= 0 && col_pair(me, mp, id, rp);
+        const bool rxp = rxn_item(me) && rxn_pair(me, mp, site[il], id, rp, site[nl]);
+#endif
+#ifdef WALK_STATS  // diagnostic build: pairs walked / within the kind pair's xy reach / passing, by kind pair
+        {
+          const int c = ((me.x & RID_LIG) ? 2 : 0) + ((id.x & RID_LIG) ? 1 : 0);
+          const float dx = rp.x - mp.x, dy = rp.y - mp.y, R = c == 0 ? 58.0f : (c == 3 ? 131.5f : 106.0f);
+          const bool xy = dx * dx + dy * dy < R * R;
+          for (int k = 0; k < 4; ++k) {
+            const uint32_t w = __popcll(__ballot(c == k)), x = __popcll(__ballot(c == k && xy)),
+                           v = __popcll(__ballot(c == k && (colp || rxp)));
+            if (__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) {
+              atomicAdd((unsigned long long*)&d.ctl->stamps[k], (unsigned long long)w);
+              atomicAdd((unsigned long long*)&d.ctl->stamps[4 + k], (unsigned long long)x);
+              atomicAdd((unsigned long long*)&d.ctl->stamps[8 + k], (unsigned long long)v);
+            }
+          }
+        }
+#endif
+#if CHK_PRED
+        bad |= colp & (id.y < 0);
+        const bool cp = colp & (id.y >= 0);
+        const uint32_t x = (uint32_t)il | (uint32_t)nl << 16;
+        if (cp & (Bc.n >= 4)) col_emit(d, Lc, tile_global(T, il), tile_global(T, nl));
+        pair_push_if(Bc, cp & (Bc.n < 4), x);
+        if (rxp & (Br.n >= 4)) rxn_emit(d, Lr, tile_global(T, il), tile_global(T, nl));
+        pair_push_if(Br, rxp & (Br.n < 4), x);
+#else
+        // (branches: most chunks have no passing pair, and the wave skips the
+        // pushes; measured faster than selects on every pair)
+        if (colp) {
+          if (id.y < 0) bad = true;
           else if (Bc.n < 4) pair_push(Bc, make_int2(il, nl));
           else col_emit(d, Lc, tile_global(T, il), tile_global(T, nl));
         }
-        if (rxn_item(me) && rxn_pair(me, mp, site[il], id, rp, site[nl])) {
+        if (rxp) {
           if (Br.n < 4) pair_push(Br, make_int2(il, nl));
           else rxn_emit(d, Lr, tile_global(T, il), tile_global(T, nl));
         }
+#endif
       });
+  if (bad) atomicOr(&d.ctl->err, ERR_RESOLVE);
   S(d, 5);
   auto glb = [&](int2 v) { return make_int2(tile_global(T, v.x), tile_global(T, v.y)); };
   pair_flush(Bc, Lc, d.cand, &d.ctl->err, glb);
@@ -3294,7 +3416,9 @@ __global__ void k_rxn_exact(KParams P, Dev d) {
   for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
     const int2 pr = sl_at(d.pairs, pre, t);
     const int2 ra = d.rec[pr.x].id, rb = d.rec[pr.y].id;
+    if (P.dbg_cand) atomicAdd(&d.ctl->rxn_kind[0], 1u);
     if (!rec_final(d, ra, step) || !rec_final(d, rb, step)) continue;  // not both final positions (see the pair scan)
+    if (P.dbg_cand) atomicAdd(&d.ctl->rxn_kind[1], 1u);
     const int i = ra.x & RID_PID, q = rb.x & RID_PID;
     if (q >= NA) {
       int lb = q - NA;
@@ -3303,6 +3427,7 @@ __global__ void k_rxn_exact(KParams P, Dev d) {
         double ddx = N.B(lb, k, 2, 0) - N.A(i, 3, 2, 0), ddy = N.B(lb, k, 2, 1) - N.A(i, 3, 2, 1),
                ddz = N.B(lb, k, 2, 2) - N.A(i, 3, 2, 2);
         if (!(d2(ddx, ddy, ddz) < P.T_bond)) continue;
+        if (P.dbg_cand) atomicAdd(&d.ctl->rxn_kind[2], 1u);
         double ot = gettheta(N.A(i, 3, 1, 0) - N.A(i, 3, 2, 0), N.A(i, 3, 1, 1) - N.A(i, 3, 2, 1),
                              N.A(i, 3, 1, 2) - N.A(i, 3, 2, 2), N.B(lb, k, 1, 0) - N.B(lb, k, 2, 0),
                              N.B(lb, k, 1, 1) - N.B(lb, k, 2, 1), N.B(lb, k, 1, 2) - N.B(lb, k, 2, 2));
@@ -3313,6 +3438,7 @@ __global__ void k_rxn_exact(KParams P, Dev d) {
         const uint64_t ri = (uint64_t)d.id_of[i], rq = (uint64_t)d.id_of[q];
         double u = kmcr::uniform(P.key, kmcr::DOM_RL, (uint32_t)ri, (uint32_t)rq, step, (uint32_t)k);
         if (!(u < P.p_ass)) continue;
+        if (P.dbg_cand) atomicAdd(&d.ctl->rxn_kind[3], 1u);
         uint32_t pos = atomicAdd(&d.ctl->n_rl, 1u);
         if (pos < d.cap_edges)
           d.rl_keys[pos] = (ri << 34) | (rq << 2) | (uint64_t)(k - 2);
@@ -3323,6 +3449,7 @@ __global__ void k_rxn_exact(KParams P, Dev d) {
       double ddx = N.A(q, 3, 3, 0) - N.A(i, 3, 3, 0), ddy = N.A(q, 3, 3, 1) - N.A(i, 3, 3, 1),
              ddz = N.A(q, 3, 3, 2) - N.A(i, 3, 3, 2);
       if (!(d2(ddx, ddy, ddz) < P.T_cis)) continue;
+      if (P.dbg_cand) atomicAdd(&d.ctl->rxn_kind[2], 1u);
       double ot = gettheta(N.A(i, 3, 1, 0) - N.A(i, 3, 3, 0), N.A(i, 3, 1, 1) - N.A(i, 3, 3, 1),
                            N.A(i, 3, 1, 2) - N.A(i, 3, 3, 2), N.A(q, 3, 1, 0) - N.A(q, 3, 3, 0),
                            N.A(q, 3, 1, 1) - N.A(q, 3, 3, 1), N.A(q, 3, 1, 2) - N.A(q, 3, 3, 2));
@@ -3332,6 +3459,7 @@ __global__ void k_rxn_exact(KParams P, Dev d) {
       double uc = kmcr::uniform(P.key, kmcr::DOM_CIS, (uint32_t)ri, (uint32_t)rq, step, 0);
       uint64_t fl = (um < P.p_mono ? 1u : 0u) | (uc < P.p_cis ? 2u : 0u);
       if (!fl) continue;
+      if (P.dbg_cand) atomicAdd(&d.ctl->rxn_kind[3], 1u);
       uint32_t pos = atomicAdd(&d.ctl->n_cisc, 1u);
       if (pos < d.cap_edges)
         d.cis_keys[pos] = (ri << 34) | (rq << 2) | fl;
@@ -3833,9 +3961,9 @@ __global__ void k_gather_beads(const double* in, double* out, const int32_t* per
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (mode == 0) {
     if (t >= (size_t)n * (ligand ? ROWS_B : ROWS_A)) return;
-    const int r = (int)(t / n), s = (int)(t % n);
-    reinterpret_cast<double2*>(out)[(size_t)r * n + s] =
-        reinterpret_cast<const double2*>(in)[(size_t)r * n + (perm[off + s] - off)];
+    const int r = (int)(t / n), s = (int)(t % n), rows = ligand ? ROWS_B : ROWS_A;
+    reinterpret_cast<double2*>(out)[bead_elem(s, r, n, rows)] =
+        reinterpret_cast<const double2*>(in)[bead_elem(perm[off + s] - off, r, n, rows)];
     return;
   }
   if (t >= (size_t)n * (ligand ? 24 : 48)) return;

@@ -13,7 +13,7 @@ oracle (cell-list mode) is advanced STEPS steps; stored:
 
 The GPU test (tests/test_gpu_long.py) regenerates the same placement on the
 host and replays the whole window.  Runs in this container (about an hour
-per 10^4 steps, one thread; the committed fixture is `make_c2_long.py 40000`);
+per 10^4 steps, one thread; the committed fixture: `make_c2_long.py 40000` and four segments, below);
 the result is data only.  The file is rewritten
 (atomically) every SAVE_EVERY steps with the steps done so far, so a long run
 (BASELINE.json C2: 10^5 steps) yields a usable, shorter fixture at any time.

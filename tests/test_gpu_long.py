@@ -1,13 +1,18 @@
-"""C2 long-horizon bit-exactness (BASELINE.json config 2: "1e5 particles ...
-fixed seed — bit-exact state counts vs CPU").
+"""C2 long-horizon bit-exactness (BASELINE.json config 2: "1e5 particles, 1e5
+steps, 1×MI355X, fixed seed — bit-exact state counts vs CPU").
 
 tests/golden/c2_long.npz holds the keyed CPU oracle's (cell-list mode) run of
 C2 (75 000 + 25 000 proteins, reference physics and density, seed 1) from the
 keyed placement: every step's bond.dat record (main.cpp:2251 columns + cluster
-sums) and the full-state hash every 100 steps, for 40 000 steps
-(tests/golden/make_c2_long.py 40000, about 3.5 hours of CPU; 2 347 bonds at the
-end, 2.5·10^6 collision rejections, 4 617 lay-downs).  The GPU replays the
-whole window here in seconds."""
+sums) and the full-state hash every 100 steps, for 10^5 steps — 6 564 bonds
+at the end, 8 639 lay-downs, 3.8·10^5 multi-ligand alignments, 6.2·10^6
+collision rejections.  Steps 0–4·10^4 are one continuous oracle run
+(make_c2_long.py 40000, 3.5 h of CPU); steps 4·10^4–10^5 are four oracle
+segments of 1.5·10^4 steps (make_c2_long.py --start-state / --save-state),
+joined by merge_c2_segments.py only because each segment's own final state is
+byte-identical to the next segment's start state (and the first start state's
+full hash equals the continuous run's at 4·10^4): every step is the oracle's.
+The GPU replays the whole window here in about a minute."""
 import os
 
 import numpy as np
@@ -34,4 +39,4 @@ def test_c2_long_horizon_matches_oracle_fixture():
         h = engine.state_hash(p, sim.get_state())
         assert h == int(g["hashes"][c]), f"state hash differs at step {(c + 1) * every}"
     assert sim.current_step == steps
-    assert steps >= 40000 and g["obs"][-1]["bond_num"] > 2000
+    assert steps >= 100000 and g["obs"][-1]["bond_num"] > 6000

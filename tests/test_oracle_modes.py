@@ -105,3 +105,25 @@ def test_cells_equal_brute_fixture_at_scale(n_a, n_b):
     assert np.array_equal(hashes, g["hashes"])
     assert np.array_equal(obs, g["obs"])
     assert obs[-1]["bond_num"] > 0
+
+
+def test_c2_long_fixture_head_and_shape():
+    # the committed C2 long-horizon fixture (tests/golden/c2_long.npz, 10^5
+    # steps, replayed on the GPU by test_gpu_long.py) starts where the keyed
+    # oracle starts today: its first 60 steps from the placement, records and
+    # hashes; every step present once and in order
+    import os
+
+    import numpy as np
+
+    from _kmc import GOLDEN, engine, workloads
+
+    g = np.load(os.path.join(GOLDEN, "c2_long.npz"), allow_pickle=False)
+    steps, every = int(g["steps"]), int(g["hash_every"])
+    assert steps >= 100000 and len(g["obs"]) == steps and len(g["hashes"]) == steps // every
+    assert np.array_equal(g["obs"]["step"], np.arange(1, steps + 1))
+    p = workloads.params("C2", seed=int(g["seed"]))
+    o = O.Oracle(p, rng_mode=O.RNG_KEYED, nbmode=O.NB_CELLS)
+    o.set_state(engine.host_init_random(p))
+    obs, _ = o.step(60, want_hashes=False)
+    assert np.array_equal(obs, g["obs"][:60])
