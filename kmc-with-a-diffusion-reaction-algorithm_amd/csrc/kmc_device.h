@@ -105,7 +105,7 @@ enum : uint32_t { S_ACC = 1, S_PEND = 2, S_REJ = 3 };  // unit fate this step (a
 // slots form one contiguous run (rows × 1 KiB) rather than `rows` streams n
 // elements apart; the buffers then hold a whole number of 64-slot blocks.
 #ifndef BEAD_BLOCK
-#define BEAD_BLOCK 0
+#define BEAD_BLOCK 1
 #endif
 __host__ __device__ __forceinline__ size_t bead_elem(int i, int r, int n, int rows) {
 #if BEAD_BLOCK

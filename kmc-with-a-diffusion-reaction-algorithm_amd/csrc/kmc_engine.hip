@@ -323,6 +323,7 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   rc |= dalloc(s, &d.cx_off, NB);
   rc |= dalloc(s, &d.cx_size, NB);
   rc |= dalloc(s, &d.cx_nb, NB);
+  rc |= dalloc(s, &d.cx_ext, NB);
   d.mcap = (uint32_t)(3 * (size_t)N);
   K.cx_limit = d.mcap / 2;
   {
@@ -559,6 +560,7 @@ static int clear_step_tags(kmc_sim* s) {
   HIPCHK(s, hipMemsetAsync(d.bfs_cand, 0, sizeof(uint32_t) * (size_t)s->K.NB, st));
   HIPCHK(s, hipMemsetAsync(d.shuf_tag, 0, sizeof(uint32_t) * (size_t)s->K.NB, st));
   HIPCHK(s, hipMemsetAsync(d.tout_n, 0, sizeof(uint32_t) * (size_t)s->ntiles, st));
+  HIPCHK(s, hipMemsetAsync(d.cx_ext, 0, sizeof(uint32_t) * (size_t)s->K.NB, st));
   return KMC_OK;
 }
 
@@ -1030,9 +1032,11 @@ int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out) {
               (unsigned long long)t[10], (unsigned long long)t[3], (unsigned long long)t[7], (unsigned long long)t[11]);
 #endif
       if (t[16])
-        fprintf(stderr, "kmc stamps cx stage %llu rigid %llu checks %llu writeback %llu count %llu next %llu\n",
+        fprintf(stderr, "kmc stamps heavy stage %llu align %llu writeback %llu records %llu (cycles summed over "
+                "waves) complexes %llu max-cycles %llu members %llu\n",
                 (unsigned long long)t[16], (unsigned long long)t[17], (unsigned long long)t[18],
-                (unsigned long long)t[19], (unsigned long long)t[20], (unsigned long long)t[21]);
+                (unsigned long long)t[19], (unsigned long long)t[20], (unsigned long long)t[21],
+                (unsigned long long)t[22]);
       if (t[0] | t[8])
         fprintf(stderr, "kmc stamps col %llu %llu %llu %llu %llu %llu %llu %llu rxn %llu %llu %llu %llu %llu %llu %llu %llu\n",
                 (unsigned long long)t[0], (unsigned long long)t[1], (unsigned long long)t[2], (unsigned long long)t[3],

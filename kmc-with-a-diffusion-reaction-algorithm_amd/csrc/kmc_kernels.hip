@@ -55,6 +55,8 @@ struct Dev {
   int32_t* cx_off;   // [NB]
   int32_t* cx_size;  // [NB]
   int32_t* cx_nb;    // [NB] ligands in complex
+  uint32_t* cx_ext;  // [NB] by root: a member of the complex broke the extent bound in k_move_members (k_cx_check
+                     // reads and clears it)
   int32_t* members;  // [mcap] BFS rows of the registered complexes (kept across steps, BFS order)
   int32_t* shuf;     // [mcap] the rows after this step's multi-ligand shuffles (cluster.log)
   int4* mrec;        // [mcap] member records of rows of <= CXL members (register_complex)
@@ -1582,33 +1584,73 @@ __device__ __forceinline__ int cx_stage_mrec(const Dev& d, CxLds* L, int off, in
   return r.x;
 }
 
-// R_new rows of every staged member (paired layout, kmc_device.h), and the
-// member row in its shuffled order (cluster.log, main.cpp:2291-2305)
-__device__ __forceinline__ void cx_write_back(const Dev& d, CxLds* L, int* grow, int csize, int nB, int NA, int lane) {
-  for (int q = 0; q < csize; ++q) {
-    const int m = L->slot[q];
-    const double* b = L->bead[q];
-    if (m < NA) {
-      if (lane < ROWS_A) {
-        double2 v;
-        if (lane < 16) {
-          v = make_double2(b[lane * 3], b[lane * 3 + 1]);
-        } else {
-          const int h = (lane - 16) >> 2, kk = (lane - 16) & 3;
-          v = make_double2(b[((2 * h) * 4 + kk) * 3 + 2], b[((2 * h + 1) * 4 + kk) * 3 + 2]);
-        }
-        d.nxt.A2(m, lane) = v;
+// bead (LDS image) of a staged member's R_new row: receptor rows 0..15 are
+// (x, y) of bead `row`, 16..23 the z of beads (2h)·4 + kk and (2h+1)·4 + kk;
+// ligand rows 0..7 and 8..11 likewise with 2 beads per j (kmc_device.h)
+__device__ __forceinline__ void cx_row_beads(bool lig, int row, int& b0, int& b1, bool& xy) {
+  const int nk = lig ? 2 : 4, nxy = 4 * nk;
+  xy = row < nxy;
+  const int h = (row - nxy) / nk, kk = (row - nxy) % nk;
+  b0 = xy ? row : (2 * h) * nk + kk;
+  b1 = (2 * h + 1) * nk + kk;
+}
+
+// R_new rows of every staged member into the LDS image: each lane takes
+// (member, row) pairs of all members at once, every load in flight before
+// the LDS stores
+__device__ __forceinline__ void cx_load_beads(const Dev& d, CxLds* L, int csize, int NA, int lane) {
+  constexpr int IT = 3;  // loads in flight per lane (two rounds cover CXL · ROWS_A = 384 rows)
+  for (int e0 = 0; e0 < csize * ROWS_A; e0 += IT * 64) {
+  double2 v[IT];
+  int qi[IT];  // member | row << 8 | ligand << 16, or -1
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int e = e0 + lane + it * 64, q = e / ROWS_A, row = e - q * ROWS_A;
+    qi[it] = -1;
+    if (q < csize) {
+      const int m = L->slot[q];
+      if (m < NA) {
+        v[it] = d.nxt.A2(m, row);
+        qi[it] = q | row << 8;
+      } else if (row < ROWS_B) {
+        v[it] = d.nxt.B2(m - NA, row);
+        qi[it] = q | row << 8 | 1 << 16;
       }
-    } else if (lane < ROWS_B) {
-      double2 v;
-      if (lane < 8) {
-        v = make_double2(b[lane * 3], b[lane * 3 + 1]);
-      } else {
-        const int h = (lane - 8) >> 1, kk = (lane - 8) & 1;
-        v = make_double2(b[((2 * h) * 2 + kk) * 3 + 2], b[((2 * h + 1) * 2 + kk) * 3 + 2]);
-      }
-      d.nxt.B2(m - NA, lane) = v;
     }
+  }
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    if (qi[it] < 0) continue;
+    int b0, b1;
+    bool xy;
+    cx_row_beads(qi[it] >> 16, (qi[it] >> 8) & 0xff, b0, b1, xy);
+    double* b = L->bead[qi[it] & 0xff];
+    if (xy) {
+      b[b0 * 3] = v[it].x;
+      b[b0 * 3 + 1] = v[it].y;
+    } else {
+      b[b0 * 3 + 2] = v[it].x;
+      b[b1 * 3 + 2] = v[it].y;
+    }
+  }
+  }
+}
+
+// R_new rows of every staged member (paired layout, kmc_device.h), (member,
+// row) pairs of all members at once, and the member row in its shuffled
+// order (cluster.log, main.cpp:2291-2305)
+__device__ __forceinline__ void cx_write_back(const Dev& d, CxLds* L, int* grow, int csize, int nB, int NA, int lane) {
+  for (int e = lane; e < csize * ROWS_A; e += 64) {
+    const int q = e / ROWS_A, row = e - q * ROWS_A, m = L->slot[q];
+    const bool lig = m >= NA;
+    if (lig && row >= ROWS_B) continue;
+    int b0, b1;
+    bool xy;
+    cx_row_beads(lig, row, b0, b1, xy);
+    const double* b = L->bead[q];
+    const double2 v = xy ? make_double2(b[b0 * 3], b[b0 * 3 + 1]) : make_double2(b[b0 * 3 + 2], b[b1 * 3 + 2]);
+    if (lig) d.nxt.B2(m - NA, row) = v;
+    else d.nxt.A2(m, row) = v;
   }
   if (nB > 1 && lane < csize) {
     const int e = L->res[lane];
@@ -1618,7 +1660,8 @@ __device__ __forceinline__ void cx_write_back(const Dev& d, CxLds* L, int* grow,
 
 // the staged members' new records (reference point from LDS; the old ones
 // were written by k_move_members), and the extent bound of the proposals
-__device__ __forceinline__ void cx_put_new(const KParams& P, const Dev& d, CxLds* L, int csize, int lane, int own) {
+__device__ __forceinline__ void cx_put_new(const KParams& P, const Dev& d, CxLds* L, int csize, int lane, int own,
+                                           uint2 home, int st) {
   if (lane >= csize) return;
   const int m = L->slot[lane];
   const double* b = L->bead[lane];
@@ -1640,7 +1683,7 @@ __device__ __forceinline__ void cx_put_new(const KParams& P, const Dev& d, CxLds
     sx = b[(2 * 4 + 2) * 3];
     sy = b[(2 * 4 + 2) * 3 + 1];
   }
-  put_rec(P, d, d.home[m], m, 1, rec_status(P, d, m), own, b[0], b[1], zl, zh, sx, sy);
+  put_rec(P, d, home, m, 1, st, own, b[0], b[1], zl, zh, sx, sy);
 }
 
 // Rigid move of one complex, main.cpp:974-1131.  Lane = (member ql of a pass
@@ -1864,7 +1907,7 @@ __device__ __forceinline__ void cx_params(const KParams& P, const Dev& d, uint32
 // units; compile-time row indices keep them in registers); the old record is
 // counted here, the new one by k_cx_check / k_complex_heavy
 template <bool IS_A>
-__device__ __forceinline__ void move_member(const KParams& P, const Dev& d, int i, const double* cp) {
+__device__ __forceinline__ void move_member(const KParams& P, const Dev& d, int i, const double* cp, int root) {
   constexpr int NK = IS_A ? 4 : 2, ROWS = IS_A ? ROWS_A : ROWS_B;
   const int n = IS_A ? P.NA : P.NB, p = IS_A ? i : P.NA + i;
   const double2* src = reinterpret_cast<const double2*>(IS_A ? d.cur.a : d.cur.b);
@@ -1909,6 +1952,17 @@ __device__ __forceinline__ void move_member(const KParams& P, const Dev& d, int 
 #pragma unroll
   for (int w = 0; w < ROWS; ++w) st_n(dst[bead_elem(i, w, n, ROWS)], r[w]);
   recs(1);
+  // the extent bound of the proposal (DESIGN.md §cell list) from registers:
+  // [j][1] xy (rows (j-1)·NK) within 0.3 Å (receptor) / 35 Å (ligand) of
+  // [1][1]; k_cx_check raises it for the complexes whose tests pass (the
+  // others are realigned by k_complex_heavy, which checks its own result)
+  bool ext = true;
+#pragma unroll
+  for (int j = 1; j < 4; ++j) {
+    const double ex = r[j * NK].x - r[0].x, ey = r[j * NK].y - r[0].y;
+    ext &= IS_A ? ex * ex + ey * ey <= 0.09 : ex * ex + ey * ey <= 35.0 * 35.0;
+  }
+  if (!ext) atomicOr(&d.cx_ext[root - P.NA], 1u);
 }
 
 __global__ void __launch_bounds__(256) k_cx_check(KParams P, Dev d) {
@@ -1920,6 +1974,8 @@ __global__ void __launch_bounds__(256) k_cx_check(KParams P, Dev d) {
     if (!cx_current(d, desc)) continue;
     const int csize = desc.z & 0xffff, nB = desc.z >> 16;
     if (csize > CXL) continue;
+    const uint32_t xb = d.cx_ext[desc.x & CXD_LB];  // (set by k_move_members, cleared here)
+    if (xb) d.cx_ext[desc.x & CXD_LB] = 0u;
     bool heavy = nB != 1;
     if (!heavy) {
       const int lb = desc.x;  // the root: the complex's only ligand
@@ -1936,21 +1992,7 @@ __global__ void __launch_bounds__(256) k_cx_check(KParams P, Dev d) {
       d.cx_heavy[atomicAdd(&d.ctl->n_heavy, 1u)] = make_int4(desc.x | CXD_MOVED, desc.y, desc.z, desc.w);
       continue;
     }
-    const int* row = d.members + desc.y;
-    for (int t = 0; t < csize; ++t) {  // the extent bound of the members' proposals (records: k_move_members)
-      const int m = row[t];
-      const bool isA = m < NA;
-      double2 b[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = isA ? N.Axy(m, j + 1, 1) : N.Bxy(m - NA, j + 1, 1);
-      bool ext = true;
-#pragma unroll
-      for (int j = 1; j < 4; ++j) {
-        const double ex = b[j].x - b[0].x, ey = b[j].y - b[0].y;
-        ext &= isA ? ex * ex + ey * ey <= 0.09 : ex * ex + ey * ey <= 35.0 * 35.0;
-      }
-      if (!ext) atomicOr(&d.ctl->err, ERR_GEOMETRY);
-    }
+    if (xb) atomicOr(&d.ctl->err, ERR_GEOMETRY);  // a member's proposal broke the extent bound
   }
 }
 
@@ -1960,7 +2002,10 @@ __global__ void __launch_bounds__(256) k_cx_check(KParams P, Dev d) {
 // move and the alignment on global memory.  Block 0's first wave first runs
 // the BFS of the components that overflowed k_bfs's LDS queue (> BFS_QCAP
 // members) and moves those it roots.  Launched after k_cx_check on its stream.
-__global__ void __launch_bounds__(256) k_complex_heavy(KParams P, Dev d) {
+#ifndef HEAVY_WAVES  // minimum waves per SIMD of k_complex_heavy (the register budget: 2 = 256, 3 = 168 VGPRs)
+#define HEAVY_WAVES 2
+#endif
+__global__ void __launch_bounds__(256, HEAVY_WAVES) k_complex_heavy(KParams P, Dev d) {
   __shared__ CxLds lds[4];
   const int lane = __lane_id(), NA = P.NA, NB = P.NB;
   CxLds* L = &lds[threadIdx.x >> 6];
@@ -1998,6 +2043,19 @@ __global__ void __launch_bounds__(256) k_complex_heavy(KParams P, Dev d) {
   const uint32_t n = d.ctl->n_heavy;
   const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
   for (uint32_t c = w; c < n; c += nw) {
+#ifdef KMC_STAMPS  // diagnostic build: per-phase cycles of the staged path (lane 0 of each wave)
+    uint64_t t0_ = Stamper::now(), t_ = t0_;
+#define CXS(i)                                                                                   \
+  do {                                                                                           \
+    if (lane == 0) {                                                                             \
+      const uint64_t v_ = Stamper::now();                                                        \
+      atomicAdd((unsigned long long*)&d.ctl->stamps[16 + (i)], (unsigned long long)(v_ - t_)); \
+      t_ = v_;                                                                                   \
+    }                                                                                            \
+  } while (0)
+#else
+#define CXS(i)
+#endif
     const int4 desc = d.cx_heavy[c];
     const int lb = desc.x & CXD_LB;
     if (!(desc.x & CXD_MOVED)) {
@@ -2005,16 +2063,16 @@ __global__ void __launch_bounds__(256) k_complex_heavy(KParams P, Dev d) {
       continue;
     }
     const int csize = desc.z & 0xffff, nB = desc.z >> 16;
-    cx_stage_mrec(d, L, desc.y, csize, NA, lane);
-    wave_sync();
-    for (int e = lane; e < csize * 16; e += 64) {  // the moved beads back into LDS
-      const int q = e >> 4, m = L->slot[q], bj = ((e >> 2) & 3) + 1, bk = (e & 3) + 1;
-      if (bk > (m < NA ? 4 : 2)) continue;
-      double* b = &L->bead[q][((bj - 1) * (m < NA ? 4 : 2) + (bk - 1)) * 3];
-      b[0] = d.nxt.P(m, bj, bk, 0);
-      b[1] = d.nxt.P(m, bj, bk, 1);
-      b[2] = d.nxt.P(m, bj, bk, 2);
+    const int mslot = cx_stage_mrec(d, L, desc.y, csize, NA, lane);
+    // this lane's member's record inputs (cx_put_new), loaded here, long before use
+    uint2 mhome = make_uint2(0u, 0u);
+    int mst = 0;
+    if (mslot >= 0) {
+      mhome = d.home[mslot];
+      mst = rec_status(P, d, mslot);
     }
+    wave_sync();
+    cx_load_beads(d, L, csize, NA, lane);  // the moved beads back into LDS
     if (nB > 1)  // the shuffles' keyed draws, all at once (main.cpp:1285, 1345, 1413, 1597)
       for (int e = lane; e < CX_SHUF * CXL; e += 64) {
         const int call = e / CXL, pos = e % CXL;
@@ -2022,6 +2080,7 @@ __global__ void __launch_bounds__(256) k_complex_heavy(KParams P, Dev d) {
           L->rnd[call][pos] = kmcr::rand31(P.key, kmcr::DOM_SHUF, (uint32_t)desc.w, call, step, pos);
       }
     wave_sync();
+    CXS(0);
     {
       // the last receptor in member order: the highest lane holding one
       const uint64_t rm = __ballot(lane < csize && L->slot[lane] < NA);
@@ -2035,10 +2094,21 @@ __global__ void __launch_bounds__(256) k_complex_heavy(KParams P, Dev d) {
         complex_align_wave(X, L, nB, pA, lane);  // the root is member 0
       }
     }
+    CXS(1);
     cx_write_back(d, L, d.shuf + desc.y, csize, nB, NA, lane);  // shuffled row: shuf (members keeps BFS order)
     if (nB > 1 && lane == 0) d.shuf_tag[lb] = step;
-    cx_put_new(P, d, L, csize, lane, desc.w);
+    CXS(2);
+    cx_put_new(P, d, L, csize, lane, desc.w, mhome, mst);
     wave_sync();
+    CXS(3);
+#ifdef KMC_STAMPS
+    if (lane == 0) {
+      atomicAdd((unsigned long long*)&d.ctl->stamps[20], 1ull);
+      atomicMax((unsigned long long*)&d.ctl->stamps[21], (unsigned long long)(t_ - t0_));
+      atomicAdd((unsigned long long*)&d.ctl->stamps[22], (unsigned long long)csize);
+    }
+#endif
+#undef CXS
   }
 }
 
@@ -2062,21 +2132,27 @@ __device__ __forceinline__ void propose_one(const KParams& P, const Dev& d, int 
 
 // member p of a complex of at most CXL members (cx_params), one thread per
 // slot: a separate launch keeps the free units' kernel at 4 waves/SIMD
-__global__ void __launch_bounds__(256) k_move_members(KParams P, Dev d) {
+#ifndef MEMBER_WAVES  // minimum waves per SIMD of k_move_members
+#define MEMBER_WAVES 1
+#endif
+__global__ void __launch_bounds__(256, MEMBER_WAVES) k_move_members(KParams P, Dev d) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x, NA = P.NA;
   if (p >= P.N) return;
   const int r = d.croot[p];
   if (r < 0 || d.cx_size[r - NA] > CXL) return;
   const double* cp = d.cxp + (size_t)(r - NA) * CXP;
-  if (p < NA) move_member<true>(P, d, p, cp);
-  else move_member<false>(P, d, p - NA, cp);
+  if (p < NA) move_member<true>(P, d, p, cp, r);
+  else move_member<false>(P, d, p - NA, cp, r);
 }
 
 // the free units, one thread per slot
 // The complexes' rigid-move parameters (cx_params) run in the first gC
 // workgroups, ahead of the free units: their short dependent chains of loads
 // overlap the free units' HBM stream instead of taking a launch of their own.
-__global__ void __launch_bounds__(256) k_propose_free(KParams P, Dev d, int gC) {
+#ifndef FREE_WAVES  // minimum waves per SIMD of k_propose_free
+#define FREE_WAVES 1
+#endif
+__global__ void __launch_bounds__(256, FREE_WAVES) k_propose_free(KParams P, Dev d, int gC) {
   if ((int)blockIdx.x < gC) {
     cx_params(P, d, blockIdx.x * blockDim.x + threadIdx.x, (uint32_t)gC * blockDim.x);
     return;
