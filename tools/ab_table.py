@@ -1,4 +1,4 @@
-"""Table of an A/B directory (tools/gpu_ab3.sh): ms/step (steady, fresh) and
+"""Table of an A/B directory of round 4's first session (made by the former tools/gpu_ab3.sh; tools/pmc_ab.py prints its own): ms/step (steady, fresh) and
 per-launch kernel means (µs) from each bench's --profile breakdown."""
 import glob
 import json
