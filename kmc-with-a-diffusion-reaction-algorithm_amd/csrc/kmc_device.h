@@ -107,10 +107,26 @@ enum : uint32_t { S_ACC = 1, S_PEND = 2, S_REJ = 3 };  // unit fate this step (a
 #ifndef BEAD_BLOCK
 #define BEAD_BLOCK 1
 #endif
+#ifndef ROW_PERM  // (A/B builds) blocked layout: the rows the gathers read first in each block
+#define ROW_PERM 0
+#endif
+__host__ __device__ __forceinline__ int bead_row(int r, int rows) {
+#if ROW_PERM
+  // receptor: [j][1] xy (0, 4, 8, 12) and their z pairs (16, 20) — the exact
+  // collision test — then the [3][k] rows of the reaction gates, then the rest;
+  // ligand: [j][1] xy (0, 2, 4, 6) and z (8, 10) first
+  constexpr unsigned char PA[24] = {0, 6, 7, 8, 1, 9, 10, 11, 2, 12, 13, 14, 3, 15, 16, 17, 4, 18, 19, 20, 5, 21, 22, 23};
+  constexpr unsigned char PB[12] = {0, 6, 1, 7, 2, 8, 3, 9, 4, 10, 5, 11};
+  return rows == 24 ? PA[r] : PB[r];
+#else
+  (void)rows;
+  return r;
+#endif
+}
 __host__ __device__ __forceinline__ size_t bead_elem(int i, int r, int n, int rows) {
 #if BEAD_BLOCK
   (void)n;
-  return ((size_t)(i >> 6) * rows + r) * 64 + (i & 63);
+  return ((size_t)(i >> 6) * rows + bead_row(r, rows)) * 64 + (i & 63);
 #else
   (void)rows;
   return (size_t)r * n + i;

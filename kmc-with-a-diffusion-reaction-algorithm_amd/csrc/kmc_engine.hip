@@ -36,6 +36,11 @@ struct kmc_sim {
   Dev d;
   int device = 0;
   hipStream_t stream = nullptr;
+  // the rejected units' R -> R_new revert runs on a second stream beside the
+  // reaction / observable kernels (neither reads what it writes); the step's
+  // end waits for it (REJ_SIDE)
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int64_t step_done = 0;
   std::string err;
   int ncell = 0;
@@ -239,7 +244,10 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
     delete s;
     return KMC_ERR_NODEVICE;
   }
-  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming) != hipSuccess) {
     kmc_destroy(s);
     return KMC_ERR_HIP;
   }
@@ -466,6 +474,9 @@ int kmc_destroy(kmc_sim* s) {
     if (e) (void)hipEventDestroy(e);
   for (auto& g : s->graphs)
     if (g.exec) (void)hipGraphExecDestroy(g.exec);
+  if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);
+  if (s->ev_join) (void)hipEventDestroy(s->ev_join);
+  if (s->side) (void)hipStreamDestroy(s->side);
   if (s->stream) (void)hipStreamDestroy(s->stream);
   delete s;
   return KMC_OK;
@@ -841,7 +852,16 @@ static int launch_step(kmc_sim* s, bool re_sort) {
     k_col_units<<<gX, T, 0, st>>>(K, d, 0);
     k_col_tail<<<1, 1024, 0, st>>>(K, d, 1);
   });
+#if REJ_SIDE
+  // fork: the revert on the side stream (k_rxn_exact reads each protein's
+  // final position from R or R_new by its record, not the reverted R_new)
+  HIPCHK(s, hipEventRecord(s->ev_fork, st));
+  HIPCHK(s, hipStreamWaitEvent(s->side, s->ev_fork, 0));
+  TIMED_ON(KI_COMMIT, s->side, (k_rej_commit<<<gX, T, 0, s->side>>>(K, d)));
+  HIPCHK(s, hipEventRecord(s->ev_join, s->side));
+#else
   TIMED(KI_COMMIT, (k_rej_commit<<<gX, T, 0, st>>>(K, d)));
+#endif
   if (K.NA > 0) {
     TIMED(KI_RXN_EXACT, (k_rxn_exact<<<1024, T, 0, st>>>(K, d)));
     TIMED(KI_MATCH, (k_match<<<1, 1024, 0, st>>>(K, d)));
@@ -850,6 +870,9 @@ static int launch_step(kmc_sim* s, bool re_sort) {
     k_diss_observe<<<gN, T, 0, st>>>(K, d);
     k_finalize<<<1, 256, 0, st>>>(K, d, s->p.time_step, gN);
   });
+#if REJ_SIDE
+  HIPCHK(s, hipStreamWaitEvent(st, s->ev_join, 0));  // join: the next step reads R
+#endif
   if (s->tnow) s->tslot = (s->tslot + 1) % TRING;
   // R_new becomes R (main.cpp:2164-2191): swap the bead buffers
   std::swap(d.cur, d.nxt);

@@ -3280,6 +3280,12 @@ __device__ __forceinline__ void rej_copy(const KParams& P, const Dev& d, int m, 
 #ifndef REJ_LANES
 #define REJ_LANES 16
 #endif
+#ifndef REJ_SIDE  // k_rej_commit on a second stream beside k_rxn_exact .. k_finalize (kmc_engine.hip)
+#define REJ_SIDE 0
+#endif
+#ifndef REJ_UNROLL  // rejected units whose lookups a lane group has in flight at once
+#define REJ_UNROLL 1
+#endif
 __global__ void k_rej_commit(KParams P, Dev d) {
   const int NA = P.NA;
   __shared__ uint32_t pre[NSHARD + 1];
@@ -3287,19 +3293,41 @@ __global__ void k_rej_commit(KParams P, Dev d) {
   const int lane = threadIdx.x % REJ_LANES;
   const uint32_t w0 = (blockIdx.x * blockDim.x + threadIdx.x) / REJ_LANES,
                  nw = (gridDim.x * blockDim.x) / REJ_LANES;
-  for (uint32_t t = w0; t < n; t += nw) {
-    const int sl = d.slot_of[sl_at(d.rej, pre, t).x];
-    const uint8_t kind = d.ukind[sl];
-    int off = 0, nm = 1, q = -1;
-    if (kind == U_COMPLEX) {
-      off = d.cx_off[sl - NA];
-      nm = d.cx_size[sl - NA];
-    } else if (kind == U_DIMER) {
-      nm = 2;
-      q = A_NEI3(d, sl) - 1;
+  constexpr int U = REJ_UNROLL;
+  // REJ_UNROLL units per pass: each step of their lookup chains (unit ->
+  // slot -> kind -> members) issued for all of them before the next, so a
+  // group waits for one chain per pass, not one per unit
+  for (uint32_t t0 = w0; t0 < n; t0 += nw * U) {
+    int sl[U], off[U], nm[U], q[U];
+    uint8_t kind[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t t = t0 + (uint32_t)u * nw;
+      sl[u] = t < n ? sl_at(d.rej, pre, t).x : -1;
     }
-    auto member = [&](int k) { return kind == U_COMPLEX ? d.members[off + k] : (k ? q : sl); };
-    for (int e = lane; e < nm * ROWS_A; e += REJ_LANES) rej_copy(P, d, member(e / ROWS_A), e % ROWS_A);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (sl[u] >= 0) sl[u] = d.slot_of[sl[u]];
+#pragma unroll
+    for (int u = 0; u < U; ++u) kind[u] = sl[u] >= 0 ? d.ukind[sl[u]] : (uint8_t)U_NONE;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      off[u] = 0;
+      nm[u] = sl[u] >= 0 ? 1 : 0;
+      q[u] = -1;
+      if (kind[u] == U_COMPLEX) {
+        off[u] = d.cx_off[sl[u] - NA];
+        nm[u] = d.cx_size[sl[u] - NA];
+      } else if (kind[u] == U_DIMER) {
+        nm[u] = 2;
+        q[u] = A_NEI3(d, sl[u]) - 1;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      auto member = [&](int k) { return kind[u] == U_COMPLEX ? d.members[off[u] + k] : (k ? q[u] : sl[u]); };
+      for (int e = lane; e < nm[u] * ROWS_A; e += REJ_LANES) rej_copy(P, d, member(e / ROWS_A), e % ROWS_A);
+    }
   }
 }
 
@@ -3486,7 +3514,6 @@ __global__ void __launch_bounds__(256, PAIR_WAVES) k_pair_scan(KParams P, Dev d)
 __global__ void k_rxn_exact(KParams P, Dev d) {
   const int NA = P.NA, NB = P.NB;
   const uint32_t step = d.ctl->step;
-  const Beads& N = d.nxt;
   __shared__ uint32_t pre[NSHARD + 1];
   const uint32_t n = sl_prefix(d.pairs, pre);
   for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
@@ -3496,20 +3523,25 @@ __global__ void k_rxn_exact(KParams P, Dev d) {
     if (!rec_final(d, ra, step) || !rec_final(d, rb, step)) continue;  // not both final positions (see the pair scan)
     if (P.dbg_cand) atomicAdd(&d.ctl->rxn_kind[1], 1u);
     const int i = ra.x & RID_PID, q = rb.x & RID_PID;
+    // final positions: the proposal (R_new) of an accepted unit, R of a
+    // rejected one — read where they are, so that k_rej_commit's R -> R_new
+    // revert may run at the same time (REJ_SIDE)
+    const Beads& NI = ra.x < 0 ? d.nxt : d.cur;
+    const Beads& NQ = rb.x < 0 ? d.nxt : d.cur;
     if (q >= NA) {
       int lb = q - NA;
       for (int k = 2; k <= 4; ++k) {
         if (B_ST(d, lb, k) != 0) continue;
-        double ddx = N.B(lb, k, 2, 0) - N.A(i, 3, 2, 0), ddy = N.B(lb, k, 2, 1) - N.A(i, 3, 2, 1),
-               ddz = N.B(lb, k, 2, 2) - N.A(i, 3, 2, 2);
+        double ddx = NQ.B(lb, k, 2, 0) - NI.A(i, 3, 2, 0), ddy = NQ.B(lb, k, 2, 1) - NI.A(i, 3, 2, 1),
+               ddz = NQ.B(lb, k, 2, 2) - NI.A(i, 3, 2, 2);
         if (!(d2(ddx, ddy, ddz) < P.T_bond)) continue;
         if (P.dbg_cand) atomicAdd(&d.ctl->rxn_kind[2], 1u);
-        double ot = gettheta(N.A(i, 3, 1, 0) - N.A(i, 3, 2, 0), N.A(i, 3, 1, 1) - N.A(i, 3, 2, 1),
-                             N.A(i, 3, 1, 2) - N.A(i, 3, 2, 2), N.B(lb, k, 1, 0) - N.B(lb, k, 2, 0),
-                             N.B(lb, k, 1, 1) - N.B(lb, k, 2, 1), N.B(lb, k, 1, 2) - N.B(lb, k, 2, 2));
-        double pd = gettheta(N.A(i, 3, 1, 0) - N.A(i, 3, 4, 0), N.A(i, 3, 1, 1) - N.A(i, 3, 4, 1),
-                             N.A(i, 3, 1, 2) - N.A(i, 3, 4, 2), N.B(lb, 1, 1, 0) - N.B(lb, 1, 2, 0),
-                             N.B(lb, 1, 1, 1) - N.B(lb, 1, 2, 1), N.B(lb, 1, 1, 2) - N.B(lb, 1, 2, 2));
+        double ot = gettheta(NI.A(i, 3, 1, 0) - NI.A(i, 3, 2, 0), NI.A(i, 3, 1, 1) - NI.A(i, 3, 2, 1),
+                             NI.A(i, 3, 1, 2) - NI.A(i, 3, 2, 2), NQ.B(lb, k, 1, 0) - NQ.B(lb, k, 2, 0),
+                             NQ.B(lb, k, 1, 1) - NQ.B(lb, k, 2, 1), NQ.B(lb, k, 1, 2) - NQ.B(lb, k, 2, 2));
+        double pd = gettheta(NI.A(i, 3, 1, 0) - NI.A(i, 3, 4, 0), NI.A(i, 3, 1, 1) - NI.A(i, 3, 4, 1),
+                             NI.A(i, 3, 1, 2) - NI.A(i, 3, 4, 2), NQ.B(lb, 1, 1, 0) - NQ.B(lb, 1, 2, 0),
+                             NQ.B(lb, 1, 1, 1) - NQ.B(lb, 1, 2, 1), NQ.B(lb, 1, 1, 2) - NQ.B(lb, 1, 2, 2));
         if (!((kmcm::fabs_(pd) < P.thetapd_cut) && (kmcm::fabs_(ot - 180) < P.thetaot_cut))) continue;
         const uint64_t ri = (uint64_t)d.id_of[i], rq = (uint64_t)d.id_of[q];
         double u = kmcr::uniform(P.key, kmcr::DOM_RL, (uint32_t)ri, (uint32_t)rq, step, (uint32_t)k);
@@ -3522,13 +3554,13 @@ __global__ void k_rxn_exact(KParams P, Dev d) {
           atomicOr(&d.ctl->err, ERR_EDGES);
       }
     } else {
-      double ddx = N.A(q, 3, 3, 0) - N.A(i, 3, 3, 0), ddy = N.A(q, 3, 3, 1) - N.A(i, 3, 3, 1),
-             ddz = N.A(q, 3, 3, 2) - N.A(i, 3, 3, 2);
+      double ddx = NQ.A(q, 3, 3, 0) - NI.A(i, 3, 3, 0), ddy = NQ.A(q, 3, 3, 1) - NI.A(i, 3, 3, 1),
+             ddz = NQ.A(q, 3, 3, 2) - NI.A(i, 3, 3, 2);
       if (!(d2(ddx, ddy, ddz) < P.T_cis)) continue;
       if (P.dbg_cand) atomicAdd(&d.ctl->rxn_kind[2], 1u);
-      double ot = gettheta(N.A(i, 3, 1, 0) - N.A(i, 3, 3, 0), N.A(i, 3, 1, 1) - N.A(i, 3, 3, 1),
-                           N.A(i, 3, 1, 2) - N.A(i, 3, 3, 2), N.A(q, 3, 1, 0) - N.A(q, 3, 3, 0),
-                           N.A(q, 3, 1, 1) - N.A(q, 3, 3, 1), N.A(q, 3, 1, 2) - N.A(q, 3, 3, 2));
+      double ot = gettheta(NI.A(i, 3, 1, 0) - NI.A(i, 3, 3, 0), NI.A(i, 3, 1, 1) - NI.A(i, 3, 3, 1),
+                           NI.A(i, 3, 1, 2) - NI.A(i, 3, 3, 2), NQ.A(q, 3, 1, 0) - NQ.A(q, 3, 3, 0),
+                           NQ.A(q, 3, 1, 1) - NQ.A(q, 3, 3, 1), NQ.A(q, 3, 1, 2) - NQ.A(q, 3, 3, 2));
       if (!(kmcm::fabs_(ot - 180) < P.cis_theta_cut)) continue;
       const uint64_t ri = (uint64_t)d.id_of[i], rq = (uint64_t)d.id_of[q];
       double um = kmcr::uniform(P.key, kmcr::DOM_MONO, (uint32_t)ri, (uint32_t)rq, step, 0);
