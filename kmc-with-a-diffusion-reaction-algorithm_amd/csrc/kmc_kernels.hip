@@ -653,7 +653,84 @@ __device__ __forceinline__ void put_recs_glb(const KParams& P, const Dev& d, int
 
 // free receptor, main.cpp:584-635.  All 48 coordinates are loaded (24 16-byte
 // rows) before the first store (R and R_new are distinct buffers), so a lane
-// has every load in flight at once.
+// has every load in flight at once.  FREE_HALF (A/B builds): two domains at a
+// time (12 rows in flight, fewer registers: one more wave per SIMD).
+#ifndef FREE_HALF
+#define FREE_HALF 0
+#endif
+#if FREE_HALF
+__device__ void propose_free_a(const KParams& P, const Dev& d, int i, uint32_t step) {
+  const uint2 h = d.home[i];
+  double u0, u1, u2, u3;
+  const uint32_t ri = (uint32_t)d.id_of[i];
+  kmcr::uniform2(P.key, kmcr::DOM_DIFF, ri, 0, step, 0, &u0, &u1);
+  kmcr::uniform2(P.key, kmcr::DOM_DIFF, ri, 0, step, 1, &u2, &u3);
+  double amp = P.amp_a * u0;
+  double phai = u1 * 2 * P.pai;
+  double dx = amp * kmcm::cos(phai), dy = amp * kmcm::sin(phai);
+  Rot t = euler(0, 0, (2 * u2 - 1) * P.rot_a);
+  double PBx = 0.0, PBy = 0.0;
+  double ocx[4], ocy[4], oz1[4], ncx[4], ncy[4], nz1[4], osx = 0.0, osy = 0.0, nsx = 0.0, nsy = 0.0;
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    double2 v[12];  // (x, y) rows of domains 2hh+1, 2hh+2, then their z-pair rows
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] = ld_r(d.cur.A2(i, hh * 8 + r));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[8 + k] = ld_r(d.cur.A2(i, 16 + hh * 4 + k));
+    if (hh == 0) {  // periodic shift from [1][1]
+      double o11x = v[0].x + dx, o11y = v[0].y + dy;
+      PBx = P.box_x * kmcm::round_(o11x / P.box_x);
+      PBy = P.box_y * kmcm::round_(o11y / P.box_y);
+    }
+    double nz[2][4];
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int j = 2 * hh + jj;
+      const double cx = (v[jj * 4].x + dx) - PBx;
+      const double cy = (v[jj * 4].y + dy) - PBy;
+      const double cz = jj ? v[8].y : v[8].x;
+      ocx[j] = v[jj * 4].x;
+      ocy[j] = v[jj * 4].y;
+      oz1[j] = cz;
+      ncx[j] = cx;
+      ncy[j] = cy;
+      nz1[j] = cz;
+      nz[jj][0] = cz;
+      st_n(d.nxt.A2(i, j * 4), make_double2(cx, cy));
+#pragma unroll
+      for (int k = 1; k < 4; ++k) {
+        const double ox = (v[jj * 4 + k].x + dx) - PBx;
+        const double oy = (v[jj * 4 + k].y + dy) - PBy;
+        const double oz = jj ? v[8 + k].y : v[8 + k].x;
+        const double nx = rx(t, ox, oy, oz, cx, cy, cz), ny = ry(t, ox, oy, oz, cx, cy, cz);
+        st_n(d.nxt.A2(i, j * 4 + k), make_double2(nx, ny));
+        if (j == 2 && k == 2) {  // the [3][3] cis site (reaction prefilter)
+          osx = v[jj * 4 + k].x;
+          osy = v[jj * 4 + k].y;
+          nsx = nx;
+          nsy = ny;
+        }
+        nz[jj][k] = rz(t, ox, oy, oz, cx, cy, cz);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) st_n(d.nxt.A2(i, 16 + hh * 4 + k), make_double2(nz[0][k], nz[1][k]));
+  }
+  bool ext = true;
+#pragma unroll
+  for (int j = 1; j < 4; ++j) {
+    double ex = ncx[j] - ncx[0], ey = ncy[j] - ncy[0];
+    ext &= ex * ex + ey * ey <= 0.09;
+  }
+  if (!ext) atomicOr(&d.ctl->err, ERR_GEOMETRY);
+  const int own = (int)ri;  // a free receptor is its own unit, status bits 0
+  put_rec(P, d, h, i, 0, 0, own, ocx[0], ocy[0], fmin(fmin(oz1[0], oz1[1]), fmin(oz1[2], oz1[3])),
+          fmax(fmax(oz1[0], oz1[1]), fmax(oz1[2], oz1[3])), osx, osy);
+  put_rec(P, d, h, i, 1, 0, own, ncx[0], ncy[0], fmin(fmin(nz1[0], nz1[1]), fmin(nz1[2], nz1[3])),
+          fmax(fmax(nz1[0], nz1[1]), fmax(nz1[2], nz1[3])), nsx, nsy);
+}
+#else
 __device__ void propose_free_a(const KParams& P, const Dev& d, int i, uint32_t step) {
   double r[4][4][3];
 #pragma unroll
@@ -726,6 +803,7 @@ __device__ void propose_free_a(const KParams& P, const Dev& d, int i, uint32_t s
   put_rec(P, d, h, i, 1, 0, own, ncx[0], ncy[0], fmin(fmin(nz[0][0], nz[1][0]), fmin(nz[2][0], nz[3][0])),
           fmax(fmax(nz[0][0], nz[1][0]), fmax(nz[2][0], nz[3][0])), nsx, nsy);
 }
+#endif
 
 // snap receptor a2 onto a1's cis site (x,y of all 16 beads), main.cpp:786-798
 template <class S>
@@ -803,7 +881,13 @@ __device__ __forceinline__ bool bond_misaligned(const KParams& P, const S& N, in
   return bond_mis_d(P, dd1, dd2);
 }
 
-// cis dimer lead i with partner q, main.cpp:682-865 (proposal part)
+// cis dimer lead i with partner q, main.cpp:682-865 (proposal part), and
+// both receptors' records.  The [j][1] rows of both receptors (shift, centre)
+// are loaded together, then each receptor's rows two domains at a time (12
+// rows in flight) before their stores: per-bead accessors cost a load round
+// trip per bead (R and R_new may alias for the compiler), and a dimer lead
+// held its wave ~30 round trips.  Records and the extent bound come from
+// registers, as for the free units.
 __device__ __forceinline__ void propose_dimer(const KParams& P, const Dev& d, int i, int q, uint32_t step) {
   double u0, u1, u2, u3;
   const uint32_t ri = (uint32_t)d.id_of[i];
@@ -812,37 +896,127 @@ __device__ __forceinline__ void propose_dimer(const KParams& P, const Dev& d, in
   double amp = P.amp_cis * u0;
   double phai = u1 * 2 * P.pai;
   double dx = amp * kmcm::cos(phai), dy = amp * kmcm::sin(phai);
-  double PBx = P.box_x * kmcm::round_(((d.cur.A(i, 1, 1, 0) + dx) + (d.cur.A(q, 1, 1, 0) + dx)) / 2 / P.box_x);
-  double PBy = P.box_y * kmcm::round_(((d.cur.A(i, 1, 1, 1) + dy) + (d.cur.A(q, 1, 1, 1) + dy)) / 2 / P.box_y);
-  Rot t = euler(0, 0, (2 * u2 - 1) * P.rot_cis);
-  // rotation centre: R_new before the move (= R), main.cpp:740-753
-  double cmx = 0, cmy = 0, cmz = 0;
-  for (int j = 1; j <= 4; ++j) {
-    cmx = cmx + d.cur.A(i, j, 1, 0) + d.cur.A(q, j, 1, 0);
-    cmy = cmy + d.cur.A(i, j, 1, 1) + d.cur.A(q, j, 1, 1);
-    cmz = cmz + d.cur.A(i, j, 1, 2) + d.cur.A(q, j, 1, 2);
+  double cmx = 0, cmy = 0, cmz = 0, PBx, PBy;
+  {
+    // [j][1] (x, y), z of [1,2][1] and [3,4][1], [3][3] (x, y): the shift,
+    // the centre and both old records
+    double2 ci[4], cq[4], zi[2], zq[2], si, sq;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      ci[j] = d.cur.A2(i, j * 4);
+      cq[j] = d.cur.A2(q, j * 4);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      zi[h] = d.cur.A2(i, 16 + h * 4);
+      zq[h] = d.cur.A2(q, 16 + h * 4);
+    }
+    si = d.cur.A2(i, 10);
+    sq = d.cur.A2(q, 10);
+    put_rec(P, d, d.home[i], i, 0, rec_status(P, d, i), d.owner[i], ci[0].x, ci[0].y,
+            fmin(fmin(zi[0].x, zi[0].y), fmin(zi[1].x, zi[1].y)), fmax(fmax(zi[0].x, zi[0].y), fmax(zi[1].x, zi[1].y)),
+            si.x, si.y);
+    put_rec(P, d, d.home[q], q, 0, rec_status(P, d, q), d.owner[q], cq[0].x, cq[0].y,
+            fmin(fmin(zq[0].x, zq[0].y), fmin(zq[1].x, zq[1].y)), fmax(fmax(zq[0].x, zq[0].y), fmax(zq[1].x, zq[1].y)),
+            sq.x, sq.y);
+    PBx = P.box_x * kmcm::round_(((ci[0].x + dx) + (cq[0].x + dx)) / 2 / P.box_x);
+    PBy = P.box_y * kmcm::round_(((ci[0].y + dy) + (cq[0].y + dy)) / 2 / P.box_y);
+    // rotation centre: R_new before the move (= R), main.cpp:740-753
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      cmx = cmx + ci[j].x + cq[j].x;
+      cmy = cmy + ci[j].y + cq[j].y;
+      cmz = cmz + (j & 1 ? zi[j >> 1].y : zi[j >> 1].x) + (j & 1 ? zq[j >> 1].y : zq[j >> 1].x);
+    }
   }
   cmx = cmx / (4 * 2);
   cmy = cmy / (4 * 2);
   cmz = cmz / (4 * 2);
+  Rot t = euler(0, 0, (2 * u2 - 1) * P.rot_cis);
+  double2 n31i, n33i;  // the lead's new [3][1] and [3][3] (x, y)
+#pragma unroll 1
   for (int w = 0; w < 2; ++w) {
-    int a = w ? q : i;
-    for (int j = 1; j <= 4; ++j)
-      for (int k = 1; k <= 4; ++k) {
-        double ox = (d.cur.A(a, j, k, 0) + dx) - PBx;
-        double oy = (d.cur.A(a, j, k, 1) + dy) - PBy;
-        double oz = d.cur.A(a, j, k, 2);
-        d.nxt.A(a, j, k, 0) = rx(t, ox, oy, oz, cmx, cmy, cmz);
-        d.nxt.A(a, j, k, 1) = ry(t, ox, oy, oz, cmx, cmy, cmz);
-        d.nxt.A(a, j, k, 2) = rz(t, ox, oy, oz, cmx, cmy, cmz);
+    const int a = w ? q : i;
+    double2 n11, ns, n31;
+    double zlo, zhi;  // of the new [j][1] z
+    bool ext = true;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      double2 v[12];  // (x, y) rows of domains 2h+1, 2h+2, then their z-pair rows
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] = ld_r(d.cur.A2(a, h * 8 + r));
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[8 + k] = ld_r(d.cur.A2(a, 16 + h * 4 + k));
+      double nz[2][4];
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const double ox = (v[jj * 4 + k].x + dx) - PBx;
+          const double oy = (v[jj * 4 + k].y + dy) - PBy;
+          const double oz_ = jj ? v[8 + k].y : v[8 + k].x;
+          const double2 nxy = make_double2(rx(t, ox, oy, oz_, cmx, cmy, cmz), ry(t, ox, oy, oz_, cmx, cmy, cmz));
+          nz[jj][k] = rz(t, ox, oy, oz_, cmx, cmy, cmz);
+          st_n(d.nxt.A2(a, h * 8 + jj * 4 + k), nxy);
+          if (k == 0) {  // [j][1]: reference point and extent bound (extent_ok)
+            if (h == 0 && jj == 0) {
+              n11 = nxy;
+            } else {
+              const double ex = nxy.x - n11.x, ey = nxy.y - n11.y;
+              ext &= ex * ex + ey * ey <= 0.09;
+            }
+          }
+          if (h == 1 && jj == 0 && k == 0) n31 = nxy;
+          if (h == 1 && jj == 0 && k == 2) ns = nxy;
+        }
+      if (h == 0) {
+        zlo = fmin(nz[0][0], nz[1][0]);
+        zhi = fmax(nz[0][0], nz[1][0]);
+      } else {
+        zlo = fmin(zlo, fmin(nz[0][0], nz[1][0]));
+        zhi = fmax(zhi, fmax(nz[0][0], nz[1][0]));
       }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) st_n(d.nxt.A2(a, 16 + h * 4 + k), make_double2(nz[0][k], nz[1][k]));
+    }
+    if (w == 0) {
+      n31i = n31;
+      n33i = ns;
+    } else {
+      // relax, main.cpp:770-799: dxyA on the new positions
+      double ex = n33i.x - ns.x, ey = n33i.y - ns.y;
+      const double dist2 = kmcm::sqrt_(ex * ex + ey * ey);
+      ex = n31i.x - n31.x;
+      ey = n31i.y - n31.y;
+      const double dist1 = kmcm::sqrt_(ex * ex + ey * ey);
+      const double dist3 = P.cis_cut / 2 + P.ra + P.ra;
+      const double dist4 = P.cis_cut / 2;
+      if (!AreSame(dist1, dist3) || !AreSame(dist2, dist4)) {
+        // snap the partner onto the lead's cis site (main.cpp:786-798; snap_cis
+        // on registers): every domain's beads 1 and 4 at (x1, y1), 3 at (x3,
+        // y3), 2 at (x2, y2) — its [j][1] beads coincide (extent bound holds)
+        const double RA = P.ra, cc = P.cis_cut;
+        const double x1 = (cc / 2 + RA) / RA * (n33i.x - n31i.x) + n33i.x;
+        const double y1 = (cc / 2 + RA) / RA * (n33i.y - n31i.y) + n33i.y;
+        const double x3 = (cc / 2) / RA * (n33i.x - n31i.x) + n33i.x;
+        const double y3 = (cc / 2) / RA * (n33i.y - n31i.y) + n33i.y;
+        const double x2 = (cc / 2 + 2 * RA) / RA * (n33i.x - n31i.x) + n33i.x;
+        const double y2 = (cc / 2 + 2 * RA) / RA * (n33i.y - n31i.y) + n33i.y;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          st_n(d.nxt.A2(q, j * 4), make_double2(x1, y1));
+          st_n(d.nxt.A2(q, j * 4 + 1), make_double2(x2, y2));
+          st_n(d.nxt.A2(q, j * 4 + 2), make_double2(x3, y3));
+          st_n(d.nxt.A2(q, j * 4 + 3), make_double2(x1, y1));
+        }
+        n11 = make_double2(x1, y1);
+        ns = make_double2(x3, y3);
+        ext = true;
+      }
+    }
+    put_rec(P, d, d.home[a], a, 1, rec_status(P, d, a), d.owner[a], n11.x, n11.y, zlo, zhi, ns.x, ns.y);
+    if (!ext) atomicOr(&d.ctl->err, ERR_GEOMETRY);
   }
-  // relax, main.cpp:770-799
-  double dist2 = dxyA(d.nxt, i, 3, 3, q, 3, 3);
-  double dist1 = dxyA(d.nxt, i, 3, 1, q, 3, 1);
-  double dist3 = P.cis_cut / 2 + P.ra + P.ra;
-  double dist4 = P.cis_cut / 2;
-  if (!AreSame(dist1, dist3) || !AreSame(dist2, dist4)) snap_cis(P, d.nxt, q, i, P.cis_cut);
 }
 
 // single ligand, main.cpp:905-969 (all 24 coordinates, 12 16-byte rows,
@@ -1566,9 +1740,8 @@ __device__ __forceinline__ void complex_align(const CX& X, int nB, int lbB, int 
 // LDS image of a complex (lanes < csize) from the member records
 // register_complex stored: slots and links encoded by BFS position (one
 // coalesced 16-byte load per member); returns the lane's member slot or -1
-__device__ __forceinline__ int cx_stage_mrec(const Dev& d, CxLds* L, int off, int csize, int NA, int lane) {
+__device__ __forceinline__ int cx_stage_mrec_r(CxLds* L, int4 r, int csize, int NA, int lane) {
   if (lane >= csize) return -1;
-  const int4 r = d.mrec[off + lane];
   L->slot[lane] = r.x;
   L->res[lane] = r.x < NA ? lane : NA + lane;
   L->mv[lane] = 0;
@@ -1582,6 +1755,9 @@ __device__ __forceinline__ int cx_stage_mrec(const Dev& d, CxLds* L, int off, in
     L->lk[lane][3] = r.w;
   }
   return r.x;
+}
+__device__ __forceinline__ int cx_stage_mrec(const Dev& d, CxLds* L, int off, int csize, int NA, int lane) {
+  return cx_stage_mrec_r(L, lane < csize ? d.mrec[off + lane] : make_int4(0, 0, 0, 0), csize, NA, lane);
 }
 
 // bead (LDS image) of a staged member's R_new row: receptor rows 0..15 are
@@ -1824,6 +2000,9 @@ __device__ __forceinline__ bool cx_current(const Dev& d, int4 desc) {
 }
 
 // complexes c = first, first + stride, ... of the descriptor list
+#ifndef CXP_BATCH  // members whose beads cx_params holds in registers at once (its VGPRs bound k_propose_free's)
+#define CXP_BATCH 4
+#endif
 __device__ __forceinline__ void cx_params(const KParams& P, const Dev& d, uint32_t first, uint32_t stride) {
   const uint32_t n = d.ctl->n_cx, step = d.ctl->step;
   for (uint32_t c = first; c < n; c += stride) {
@@ -1841,14 +2020,14 @@ __device__ __forceinline__ void cx_params(const KParams& P, const Dev& d, uint32
     double phai = u1 * 2 * P.pai;
     double dx = amp * kmcm::cos(phai), dy = amp * kmcm::sin(phai);
     const int* row = d.members + desc.y;
-    // [j][1] beads of four members at a time in registers, summed in member order
+    // [j][1] beads of CXP_BATCH members at a time in registers, summed in member order
     double PBx = 0, PBy = 0, cmx = 0, cmy = 0, cmz = 0;
     for (int pass = 0; pass < 2; ++pass) {
-      for (int t0 = 0; t0 < csize; t0 += 4) {
-        double2 xy[4][4];
-        double z[4][4];
+      for (int t0 = 0; t0 < csize; t0 += CXP_BATCH) {
+        double2 xy[CXP_BATCH][4];
+        double z[CXP_BATCH][4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < CXP_BATCH; ++i) {
           const int t = t0 + i;
           if (t >= csize) break;
           const int m = row[t];
@@ -1863,7 +2042,7 @@ __device__ __forceinline__ void cx_params(const KParams& P, const Dev& d, uint32
           }
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < CXP_BATCH; ++i) {
           if (t0 + i >= csize) break;
           if (pass == 0) {
             PBx = PBx + (xy[i][0].x + dx);
@@ -2002,6 +2181,9 @@ __global__ void __launch_bounds__(256) k_cx_check(KParams P, Dev d) {
 // move and the alignment on global memory.  Block 0's first wave first runs
 // the BFS of the components that overflowed k_bfs's LDS queue (> BFS_QCAP
 // members) and moves those it roots.  Launched after k_cx_check on its stream.
+#ifndef HEAVY_PREFETCH  // the next complex's descriptor and member records loaded during this one
+#define HEAVY_PREFETCH 0
+#endif
 #ifndef HEAVY_WAVES  // minimum waves per SIMD of k_complex_heavy (the register budget: 2 = 256, 3 = 168 VGPRs)
 #define HEAVY_WAVES 2
 #endif
@@ -2042,6 +2224,16 @@ __global__ void __launch_bounds__(256, HEAVY_WAVES) k_complex_heavy(KParams P, D
   }
   const uint32_t n = d.ctl->n_heavy;
   const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+#if HEAVY_PREFETCH
+  // the wave's next complex: its descriptor is loaded when this one starts,
+  // its member records while this one is aligned, so a staged complex waits
+  // for one round trip (its beads) instead of three
+  int4 desc_n = w < n ? d.cx_heavy[w] : make_int4(0, 0, 0, 0);
+  auto mrec_of = [&](int4 dn) {
+    return (dn.x & CXD_MOVED) && lane < (dn.z & 0xffff) ? d.mrec[dn.y + lane] : make_int4(0, 0, 0, 0);
+  };
+  int4 mrec_n = w < n ? mrec_of(desc_n) : make_int4(0, 0, 0, 0);
+#endif
   for (uint32_t c = w; c < n; c += nw) {
 #ifdef KMC_STAMPS  // diagnostic build: per-phase cycles of the staged path (lane 0 of each wave)
     uint64_t t0_ = Stamper::now(), t_ = t0_;
@@ -2056,14 +2248,27 @@ __global__ void __launch_bounds__(256, HEAVY_WAVES) k_complex_heavy(KParams P, D
 #else
 #define CXS(i)
 #endif
+#if HEAVY_PREFETCH
+    const int4 desc = desc_n, mrec = mrec_n;
+    const bool more = c + nw < n;
+    if (more) desc_n = d.cx_heavy[c + nw];
+#else
     const int4 desc = d.cx_heavy[c];
+#endif
     const int lb = desc.x & CXD_LB;
     if (!(desc.x & CXD_MOVED)) {
       global_path(lb);
+#if HEAVY_PREFETCH
+      if (more) mrec_n = mrec_of(desc_n);
+#endif
       continue;
     }
     const int csize = desc.z & 0xffff, nB = desc.z >> 16;
+#if HEAVY_PREFETCH
+    const int mslot = cx_stage_mrec_r(L, mrec, csize, NA, lane);
+#else
     const int mslot = cx_stage_mrec(d, L, desc.y, csize, NA, lane);
+#endif
     // this lane's member's record inputs (cx_put_new), loaded here, long before use
     uint2 mhome = make_uint2(0u, 0u);
     int mst = 0;
@@ -2080,6 +2285,9 @@ __global__ void __launch_bounds__(256, HEAVY_WAVES) k_complex_heavy(KParams P, D
           L->rnd[call][pos] = kmcr::rand31(P.key, kmcr::DOM_SHUF, (uint32_t)desc.w, call, step, pos);
       }
     wave_sync();
+#if HEAVY_PREFETCH
+    if (more) mrec_n = mrec_of(desc_n);
+#endif
     CXS(0);
     {
       // the last receptor in member order: the highest lane holding one
@@ -2113,6 +2321,12 @@ __global__ void __launch_bounds__(256, HEAVY_WAVES) k_complex_heavy(KParams P, D
 }
 
 // One thread per slot: free receptors, cis dimers, free ligands.
+// DIMER_KERNEL (A/B builds): the cis dimers in a kernel of their own (1: after
+// the free units; 2: beside them, on a second stream), so the dimer path's
+// registers do not bound k_propose_free's occupancy.
+#ifndef DIMER_KERNEL
+#define DIMER_KERNEL 0
+#endif
 __device__ __forceinline__ void propose_one(const KParams& P, const Dev& d, int p) {
   if (p >= P.N) return;
   const uint32_t step = d.ctl->step;
@@ -2120,14 +2334,18 @@ __device__ __forceinline__ void propose_one(const KParams& P, const Dev& d, int 
   uint8_t k = d.ukind[p];
   if (k == U_FREE_A) {
     propose_free_a(P, d, p, step);
-  } else if (k == U_DIMER) {
+  } else if (k == U_DIMER && !DIMER_KERNEL) {
     const int q = A_NEI3(d, p) - 1;
     propose_dimer(P, d, p, q, step);
-    put_recs_glb(P, d, p);
-    put_recs_glb(P, d, q);
   } else if (k == U_FREE_B) {
     propose_free_b(P, d, p - P.NA, p, step);
   }
+}
+
+__global__ void __launch_bounds__(256) k_propose_dimer(KParams P, Dev d) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x, NA = P.NA;
+  if (p >= NA || d.ukind[p] != U_DIMER) return;
+  propose_dimer(P, d, p, A_NEI3(d, p) - 1, d.ctl->step);
 }
 
 // member p of a complex of at most CXL members (cx_params), one thread per
@@ -2932,10 +3150,10 @@ __device__ __forceinline__ void pair_push(PairBuf& b, int2 v) {
 // the same for the lanes where `on` holds, without a branch (selects only;
 // CHK_PRED A/B builds)
 __device__ __forceinline__ void pair_push_if(PairBuf& b, bool on, uint32_t x) {
-  b.v0 = on & (b.n == 0) ? x : b.v0;
-  b.v1 = on & (b.n == 1) ? x : b.v1;
-  b.v2 = on & (b.n == 2) ? x : b.v2;
-  b.v3 = on & (b.n == 3) ? x : b.v3;
+  b.v0 = (on & (b.n == 0)) ? x : b.v0;
+  b.v1 = (on & (b.n == 1)) ? x : b.v1;
+  b.v2 = (on & (b.n == 2)) ? x : b.v2;
+  b.v3 = (on & (b.n == 3)) ? x : b.v3;
   b.n += on ? 1 : 0;
 }
 // active lanes of a wave; entries mapped through f on the way out
