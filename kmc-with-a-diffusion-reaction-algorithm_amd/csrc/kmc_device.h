@@ -85,7 +85,7 @@ enum : uint32_t {
   ERR_RECORDS = 32u,    // record buffer overflow
 };
 
-enum : uint8_t { U_NONE = 0, U_FREE_A = 1, U_DIMER = 2, U_FREE_B = 3, U_COMPLEX = 4 };
+enum : uint8_t { U_NONE = 0, U_FREE_A = 1, U_DIMER = 2, U_FREE_B = 3, U_COMPLEX = 4, U_DIMER_P = 5 };  // U_DIMER_P: a cis dimer's partner
 enum : uint32_t { S_ACC = 1, S_PEND = 2, S_REJ = 3 };  // unit fate this step (atomicMax order)
 
 // ---------------------------------------------------------------- layout

@@ -847,8 +847,13 @@ static int launch_step(kmc_sim* s, bool re_sort) {
 #elif DIMER_KERNEL == 2
     HIPCHK(s, hipStreamWaitEvent(st, s->ev_djoin, 0));
 #endif
-    if (K.NB > 0) {
+    if (K.NB > 0 || DIMER_MEMBERS == 1) {  // (the cis dimers too, DIMER_MEMBERS 1)
       TIMED(KI_MOVE_MEMBERS, (k_move_members<<<gN, T, 0, st>>>(K, d)));
+    }
+#if DIMER_MEMBERS == 2
+    TIMED(KI_PROPOSE_DIMER, (k_move_dimers<<<gA, T, 0, st>>>(K, d)));
+#endif
+    if (K.NB > 0) {
       TIMED(KI_CX_CHECK, (k_cx_check<<<gL, T, 0, st>>>(K, d)));
       TIMED(KI_CX_HEAVY, (k_complex_heavy<<<1024, T, 0, st>>>(K, d)));
     }

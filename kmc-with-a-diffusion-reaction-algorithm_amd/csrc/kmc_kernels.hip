@@ -212,7 +212,7 @@ __global__ void k_classify(KParams P, Dev d) {
       int q = n3 - 1;
       const bool lead = d.id_of[i] < d.id_of[q];  // moved at the lower reference index
       own = lead ? i : q;
-      kind = lead ? U_DIMER : U_NONE;
+      kind = lead ? U_DIMER : U_DIMER_P;
     }
   } else {
     int b = p - NA;
@@ -2144,6 +2144,125 @@ __device__ __forceinline__ void move_member(const KParams& P, const Dev& d, int 
   if (!ext) atomicOr(&d.cx_ext[root - P.NA], 1u);
 }
 
+// A cis dimer's member moved by its own thread (DIMER_MEMBERS, k_move_members),
+// main.cpp:682-865: each member draws the pair's move (the lead's keyed
+// draws), derives the shift and the centre from the [j][1] rows of both, and
+// moves its own 24 rows as a complex member does (the same expressions as
+// propose_dimer); the partner then applies the relax (main.cpp:770-799)
+// against the lead's new [3][1] and [3][3], which it computes from the lead's
+// old rows with the same move.  So the pair's rows stream like every other
+// protein's (coalesced, one thread each), and k_propose_free keeps no dimer
+// path (its registers: one more wave per SIMD).
+__device__ __forceinline__ void move_dimer_member(const KParams& P, const Dev& d, int p, bool lead) {
+  const int NA = P.NA;
+  const int o = A_NEI3(d, p) - 1, i = lead ? p : o, q = lead ? o : p;
+  const uint32_t step = d.ctl->step;
+  double u0, u1, u2, u3;
+  const uint32_t ri = (uint32_t)d.id_of[i];
+  kmcr::uniform2(P.key, kmcr::DOM_DIFF, ri, 0, step, 0, &u0, &u1);
+  kmcr::uniform2(P.key, kmcr::DOM_DIFF, ri, 0, step, 1, &u2, &u3);
+  const double amp = P.amp_cis * u0;
+  const double phai = u1 * 2 * P.pai;
+  const double dx = amp * kmcm::cos(phai), dy = amp * kmcm::sin(phai);
+  double cmx = 0, cmy = 0, cmz = 0, PBx, PBy;
+  double2 l31, l33;  // the lead's old [3][1], [3][3] (x, y) (partner: the relax)
+  double l31z, l33z;
+  {
+    double2 ci[4], cq[4], zi[2], zq[2];  // [j][1] (x, y); z of [1,2][1] and [3,4][1]
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      ci[j] = d.cur.A2(i, j * 4);
+      cq[j] = d.cur.A2(q, j * 4);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      zi[h] = d.cur.A2(i, 16 + h * 4);
+      zq[h] = d.cur.A2(q, 16 + h * 4);
+    }
+    l31 = ci[2];
+    l31z = zi[1].x;
+    PBx = P.box_x * kmcm::round_(((ci[0].x + dx) + (cq[0].x + dx)) / 2 / P.box_x);
+    PBy = P.box_y * kmcm::round_(((ci[0].y + dy) + (cq[0].y + dy)) / 2 / P.box_y);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      cmx = cmx + ci[j].x + cq[j].x;
+      cmy = cmy + ci[j].y + cq[j].y;
+      cmz = cmz + (j & 1 ? zi[j >> 1].y : zi[j >> 1].x) + (j & 1 ? zq[j >> 1].y : zq[j >> 1].x);
+    }
+  }
+  if (!lead) {
+    l33 = d.cur.A2(i, 10);
+    l33z = d.cur.A2(i, 22).x;
+  }
+  cmx = cmx / (4 * 2);
+  cmy = cmy / (4 * 2);
+  cmz = cmz / (4 * 2);
+  const Rot t = euler(0, 0, (2 * u2 - 1) * P.rot_cis);
+  const double2* src = reinterpret_cast<const double2*>(d.cur.a);
+  double2* dst = reinterpret_cast<double2*>(d.nxt.a);
+  double2 r[ROWS_A];
+#pragma unroll
+  for (int w = 0; w < ROWS_A; ++w) r[w] = ld_r(src[bead_elem(p, w, NA, ROWS_A)]);
+  const uint2 h = d.home[p];
+  const int st = rec_status(P, d, p), own = d.owner[p];
+  put_rec(P, d, h, p, 0, st, own, r[0].x, r[0].y, fmin(fmin(r[16].x, r[16].y), fmin(r[20].x, r[20].y)),
+          fmax(fmax(r[16].x, r[16].y), fmax(r[20].x, r[20].y)), r[10].x, r[10].y);
+#pragma unroll
+  for (int jp = 0; jp < 2; ++jp)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int r1 = 2 * jp * 4 + k, r2 = (2 * jp + 1) * 4 + k, rzr = 16 + jp * 4 + k;
+      const double z1 = r[rzr].x, z2 = r[rzr].y;
+      const double ox1 = (r[r1].x + dx) - PBx, oy1 = (r[r1].y + dy) - PBy;
+      const double ox2 = (r[r2].x + dx) - PBx, oy2 = (r[r2].y + dy) - PBy;
+      r[r1] = make_double2(rx(t, ox1, oy1, z1, cmx, cmy, cmz), ry(t, ox1, oy1, z1, cmx, cmy, cmz));
+      r[r2] = make_double2(rx(t, ox2, oy2, z2, cmx, cmy, cmz), ry(t, ox2, oy2, z2, cmx, cmy, cmz));
+      r[rzr] = make_double2(rz(t, ox1, oy1, z1, cmx, cmy, cmz), rz(t, ox2, oy2, z2, cmx, cmy, cmz));
+    }
+  if (!lead) {
+    // relax, main.cpp:770-799: the lead's new [3][1], [3][3] against ours
+    double ox = (l31.x + dx) - PBx, oy = (l31.y + dy) - PBy;
+    const double2 n31 = make_double2(rx(t, ox, oy, l31z, cmx, cmy, cmz), ry(t, ox, oy, l31z, cmx, cmy, cmz));
+    ox = (l33.x + dx) - PBx;
+    oy = (l33.y + dy) - PBy;
+    const double2 n33 = make_double2(rx(t, ox, oy, l33z, cmx, cmy, cmz), ry(t, ox, oy, l33z, cmx, cmy, cmz));
+    double ex = n33.x - r[10].x, ey = n33.y - r[10].y;
+    const double dist2 = kmcm::sqrt_(ex * ex + ey * ey);
+    ex = n31.x - r[8].x;
+    ey = n31.y - r[8].y;
+    const double dist1 = kmcm::sqrt_(ex * ex + ey * ey);
+    if (!AreSame(dist1, P.cis_cut / 2 + P.ra + P.ra) || !AreSame(dist2, P.cis_cut / 2)) {
+      // snap onto the lead's cis site (main.cpp:786-798, snap_cis): every
+      // domain's beads 1 and 4 at (x1, y1), 3 at (x3, y3), 2 at (x2, y2)
+      const double RA = P.ra, cc = P.cis_cut;
+      const double x1 = (cc / 2 + RA) / RA * (n33.x - n31.x) + n33.x;
+      const double y1 = (cc / 2 + RA) / RA * (n33.y - n31.y) + n33.y;
+      const double x3 = (cc / 2) / RA * (n33.x - n31.x) + n33.x;
+      const double y3 = (cc / 2) / RA * (n33.y - n31.y) + n33.y;
+      const double x2 = (cc / 2 + 2 * RA) / RA * (n33.x - n31.x) + n33.x;
+      const double y2 = (cc / 2 + 2 * RA) / RA * (n33.y - n31.y) + n33.y;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        r[j * 4] = make_double2(x1, y1);
+        r[j * 4 + 1] = make_double2(x2, y2);
+        r[j * 4 + 2] = make_double2(x3, y3);
+        r[j * 4 + 3] = make_double2(x1, y1);
+      }
+    }
+  }
+#pragma unroll
+  for (int w = 0; w < ROWS_A; ++w) st_n(dst[bead_elem(p, w, NA, ROWS_A)], r[w]);
+  put_rec(P, d, h, p, 1, st, own, r[0].x, r[0].y, fmin(fmin(r[16].x, r[16].y), fmin(r[20].x, r[20].y)),
+          fmax(fmax(r[16].x, r[16].y), fmax(r[20].x, r[20].y)), r[10].x, r[10].y);
+  bool ext = true;
+#pragma unroll
+  for (int j = 1; j < 4; ++j) {
+    const double ex = r[j * 4].x - r[0].x, ey = r[j * 4].y - r[0].y;
+    ext &= ex * ex + ey * ey <= 0.09;
+  }
+  if (!ext) atomicOr(&d.ctl->err, ERR_GEOMETRY);
+}
+
 __global__ void __launch_bounds__(256) k_cx_check(KParams P, Dev d) {
   const int NA = P.NA, NB = P.NB;
   const uint32_t n = d.ctl->n_cx;
@@ -2327,6 +2446,9 @@ __global__ void __launch_bounds__(256, HEAVY_WAVES) k_complex_heavy(KParams P, D
 #ifndef DIMER_KERNEL
 #define DIMER_KERNEL 0
 #endif
+#ifndef DIMER_MEMBERS  // the cis dimers moved by their members' threads: 1 in k_move_members, 2 in k_move_dimers
+#define DIMER_MEMBERS 0
+#endif
 __device__ __forceinline__ void propose_one(const KParams& P, const Dev& d, int p) {
   if (p >= P.N) return;
   const uint32_t step = d.ctl->step;
@@ -2334,7 +2456,7 @@ __device__ __forceinline__ void propose_one(const KParams& P, const Dev& d, int 
   uint8_t k = d.ukind[p];
   if (k == U_FREE_A) {
     propose_free_a(P, d, p, step);
-  } else if (k == U_DIMER && !DIMER_KERNEL) {
+  } else if (k == U_DIMER && !DIMER_KERNEL && !DIMER_MEMBERS) {
     const int q = A_NEI3(d, p) - 1;
     propose_dimer(P, d, p, q, step);
   } else if (k == U_FREE_B) {
@@ -2356,11 +2478,28 @@ __global__ void __launch_bounds__(256) k_propose_dimer(KParams P, Dev d) {
 __global__ void __launch_bounds__(256, MEMBER_WAVES) k_move_members(KParams P, Dev d) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x, NA = P.NA;
   if (p >= P.N) return;
+#if DIMER_MEMBERS == 1
+  if (p < NA) {
+    const uint8_t k = d.ukind[p];
+    if (k == U_DIMER || k == U_DIMER_P) {
+      move_dimer_member(P, d, p, k == U_DIMER);
+      return;
+    }
+  }
+#endif
   const int r = d.croot[p];
   if (r < 0 || d.cx_size[r - NA] > CXL) return;
   const double* cp = d.cxp + (size_t)(r - NA) * CXP;
   if (p < NA) move_member<true>(P, d, p, cp, r);
   else move_member<false>(P, d, p - NA, cp, r);
+}
+
+// the cis dimers' members, one thread per receptor slot (DIMER_MEMBERS 2)
+__global__ void __launch_bounds__(256) k_move_dimers(KParams P, Dev d) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P.NA) return;
+  const uint8_t k = d.ukind[p];
+  if (k == U_DIMER || k == U_DIMER_P) move_dimer_member(P, d, p, k == U_DIMER);
 }
 
 // the free units, one thread per slot
@@ -3252,6 +3391,9 @@ __device__ __forceinline__ void mark_rej(const Dev& d, int u, uint32_t tag) {
   if (old != (tag | S_REJ)) sl_push(d.rej, make_int2(u, 0), &d.ctl->err);  // at most once per unit
 }
 
+#ifndef COL_AA_FAST  // (A/B builds) receptor-receptor candidates load only the rows their test reads
+#define COL_AA_FAST 0
+#endif
 // Pass B: exact fp64 overlap test of each candidate (main.cpp:640-664,
 // 1798-1826).  A collision with a record whose relevance is already known
 // (own unit, or a later unit's old position) rejects u outright; one with an
@@ -3261,9 +3403,19 @@ __device__ __forceinline__ void mark_rej(const Dev& d, int u, uint32_t tag) {
 __device__ __forceinline__ void col_exact_one(const KParams& P, const Dev& d, int2 a, int2 b, uint32_t tag) {
   int m = a.x & RID_PID, u = a.y, q = b.x & RID_PID, kq = b.y;
   bool isnew = b.x < 0;
-  Own o;
-  load_own(P, d.nxt, m, o);
-  const bool hit = exact_collide(P, o, isnew ? d.nxt : d.cur, q);
+  bool hit;
+  if (COL_AA_FAST && m < P.NA && q < P.NA) {
+    // receptor against receptor: domain [1][1] against domain [1][1] only
+    // (exact_collide's first case), two rows of each instead of load_own's six
+    const Beads& Q = isnew ? d.nxt : d.cur;
+    const double2 mxy = d.nxt.Axy(m, 1, 1), mz = d.nxt.A2(m, 16), qxy = Q.Axy(q, 1, 1), qz = Q.A2(q, 16);
+    const double dx = qxy.x - mxy.x, dy = qxy.y - mxy.y, dz = qz.x - mz.x;
+    hit = d2(dx, dy, dz) < P.T_aa;
+  } else {
+    Own o;
+    load_own(P, d.nxt, m, o);
+    hit = exact_collide(P, o, isnew ? d.nxt : d.cur, q);
+  }
   if (P.dbg_cand) {
     const int kk = (m >= P.NA ? 1 : 0) + (q >= P.NA ? 1 : 0);
     atomicAdd(&d.ctl->cand_kind[2 * kk], 1u);
