@@ -354,6 +354,7 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   rc |= dalloc(s, &d.overflow, NB);
   rc |= dalloc(s, &d.cx_list, (size_t)d.mcap / 2);  // kept across steps: every registration since the last rebuild
   rc |= dalloc(s, &d.cx_heavy, NB);
+  rc |= dalloc(s, &d.dimers, NA / 2 + 1);
   rc |= dalloc(s, &s->hcnt, s->ncell + 1);
   rc |= dalloc(s, &d.hstart, s->ncell + 1);
   rc |= dalloc(s, &d.home, N);
@@ -833,18 +834,22 @@ static int launch_step(kmc_sim* s, bool re_sort) {
     }
     const int gC = K.NB > 0 ? std::min(gL, 512) : 0;  // grid-stride over the descriptor list
     const int gA = std::max(1, (K.NA + T - 1) / T);
-#if DIMER_KERNEL == 2
+#if DIMER_KERNEL == 2 || (DIMER_MEMBERS == 3 && DIMER_SIDE)
     // the cis dimers on the side stream, beside the free units (both only
     // read R and write their own proteins' R_new and records)
     HIPCHK(s, hipEventRecord(s->ev_dfork, st));
     HIPCHK(s, hipStreamWaitEvent(s->side, s->ev_dfork, 0));
+#if DIMER_KERNEL == 2
     TIMED_ON(KI_PROPOSE_DIMER, s->side, (k_propose_dimer<<<gA, T, 0, s->side>>>(K, d)));
+#else
+    TIMED_ON(KI_PROPOSE_DIMER, s->side, (k_move_dimer_list<<<std::min(gA, 256), T, 0, s->side>>>(K, d)));
+#endif
     HIPCHK(s, hipEventRecord(s->ev_djoin, s->side));
 #endif
     TIMED(KI_PROPOSE_FREE, (k_propose_free<<<gC + gN, T, 0, st>>>(K, d, gC)));
 #if DIMER_KERNEL == 1
     TIMED(KI_PROPOSE_DIMER, (k_propose_dimer<<<gA, T, 0, st>>>(K, d)));
-#elif DIMER_KERNEL == 2
+#elif DIMER_KERNEL == 2 || (DIMER_MEMBERS == 3 && DIMER_SIDE)
     HIPCHK(s, hipStreamWaitEvent(st, s->ev_djoin, 0));
 #endif
     if (K.NB > 0 || DIMER_MEMBERS == 1) {  // (the cis dimers too, DIMER_MEMBERS 1)
@@ -852,6 +857,8 @@ static int launch_step(kmc_sim* s, bool re_sort) {
     }
 #if DIMER_MEMBERS == 2
     TIMED(KI_PROPOSE_DIMER, (k_move_dimers<<<gA, T, 0, st>>>(K, d)));
+#elif DIMER_MEMBERS == 3 && !DIMER_SIDE
+    TIMED(KI_PROPOSE_DIMER, (k_move_dimer_list<<<std::min(gA, 256), T, 0, st>>>(K, d)));
 #endif
     if (K.NB > 0) {
       TIMED(KI_CX_CHECK, (k_cx_check<<<gL, T, 0, st>>>(K, d)));

@@ -70,6 +70,7 @@ struct Dev {
   uint32_t* pend;    // [N] round tag: unit still waiting (resolution pass C)
   int32_t* overflow; // [NB]
   int4* cx_list;     // [NB] descriptors of the registered complexes (kept across steps; cx_params, k_cx_check)
+  int32_t* dimers;   // [NA / 2 + 1] this step's cis-dimer leads (DIMER_MEMBERS 3)
   int4* cx_heavy;    // [NB] descriptors for k_complex_heavy: larger complexes, and those k_cx_check
                      //      moved but whose lay-down / alignment changes beads
   // Home list (§records): every protein has a home position hp in an order
@@ -193,6 +194,21 @@ __device__ __forceinline__ uint32_t wave_alloc(uint32_t* ctr, uint32_t qn) {
   return (uint32_t)__shfl((int)base, leader, 64) + pre;
 }
 
+// Where the cis dimers move (A/B builds): 0 the lead's thread in
+// k_propose_free (propose_dimer); DIMER_KERNEL 1 / 2 the lead's thread in a
+// kernel of its own after / beside it; DIMER_MEMBERS: each member's own thread
+// (move_dimer_member) — 1 in k_move_members, 2 in a sweep over the receptor
+// slots (k_move_dimers), 3 from a list k_classify compacts (k_move_dimer_list).
+#ifndef DIMER_KERNEL
+#define DIMER_KERNEL 0
+#endif
+#ifndef DIMER_MEMBERS
+#define DIMER_MEMBERS 0
+#endif
+#ifndef DIMER_SIDE  // DIMER_MEMBERS 3: the list kernel on a second stream beside k_propose_free
+#define DIMER_SIDE 0
+#endif
+
 // ================================================================ 1. classify
 // Unit kinds, main.cpp:584 (free receptor), 682-686 (cis dimer, moved at the
 // lower index), 905 (single ligand = BFS component of size 1).
@@ -213,6 +229,9 @@ __global__ void k_classify(KParams P, Dev d) {
       const bool lead = d.id_of[i] < d.id_of[q];  // moved at the lower reference index
       own = lead ? i : q;
       kind = lead ? U_DIMER : U_DIMER_P;
+#if DIMER_MEMBERS == 3
+      if (lead && d.croot[p] < 0) d.dimers[wave_slot(&d.ctl->n_dimer)] = p;
+#endif
     }
   } else {
     int b = p - NA;
@@ -2439,16 +2458,7 @@ __global__ void __launch_bounds__(256, HEAVY_WAVES) k_complex_heavy(KParams P, D
   }
 }
 
-// One thread per slot: free receptors, cis dimers, free ligands.
-// DIMER_KERNEL (A/B builds): the cis dimers in a kernel of their own (1: after
-// the free units; 2: beside them, on a second stream), so the dimer path's
-// registers do not bound k_propose_free's occupancy.
-#ifndef DIMER_KERNEL
-#define DIMER_KERNEL 0
-#endif
-#ifndef DIMER_MEMBERS  // the cis dimers moved by their members' threads: 1 in k_move_members, 2 in k_move_dimers
-#define DIMER_MEMBERS 0
-#endif
+// One thread per slot: free receptors, cis dimers (by default), free ligands.
 __device__ __forceinline__ void propose_one(const KParams& P, const Dev& d, int p) {
   if (p >= P.N) return;
   const uint32_t step = d.ctl->step;
@@ -2492,6 +2502,17 @@ __global__ void __launch_bounds__(256, MEMBER_WAVES) k_move_members(KParams P, D
   const double* cp = d.cxp + (size_t)(r - NA) * CXP;
   if (p < NA) move_member<true>(P, d, p, cp, r);
   else move_member<false>(P, d, p - NA, cp, r);
+}
+
+// the cis dimers' members from this step's list, one thread per member
+// (DIMER_MEMBERS 3): a small grid, so a wave is not held by one dimer's
+// dependent loads among 63 idle lanes of a sweep over every slot
+__global__ void __launch_bounds__(256) k_move_dimer_list(KParams P, Dev d) {
+  const uint32_t n = 2 * d.ctl->n_dimer;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    const int lead = d.dimers[e >> 1], NA = P.NA;
+    move_dimer_member(P, d, (e & 1) ? A_NEI3(d, lead) - 1 : lead, !(e & 1));
+  }
 }
 
 // the cis dimers' members, one thread per receptor slot (DIMER_MEMBERS 2)
@@ -3391,8 +3412,8 @@ __device__ __forceinline__ void mark_rej(const Dev& d, int u, uint32_t tag) {
   if (old != (tag | S_REJ)) sl_push(d.rej, make_int2(u, 0), &d.ctl->err);  // at most once per unit
 }
 
-#ifndef COL_AA_FAST  // (A/B builds) receptor-receptor candidates load only the rows their test reads
-#define COL_AA_FAST 0
+#ifndef COL_AA_FAST  // receptor-receptor candidates load only the rows their test reads
+#define COL_AA_FAST 1  // (A/B, profiles/r04/ab_r4r: k_col_exact 43.4 -> 39.1 us at C3)
 #endif
 // Pass B: exact fp64 overlap test of each candidate (main.cpp:640-664,
 // 1798-1826).  A collision with a record whose relevance is already known
@@ -4356,6 +4377,7 @@ __global__ void __launch_bounds__(256) k_finalize(KParams P, Dev d, double time_
   c->n_cisc = 0;
   c->n_outl = 0;
   c->n_dense = 0;
+  c->n_dimer = 0;
 }
 
 
