@@ -61,7 +61,6 @@ struct Ctl {
   uint32_t n_cisc;        // cis candidates
   uint32_t n_outl;        // records listed on the outlier list this step (more than a cell from home)
   uint32_t n_dense;       // blocks on the dense list this step (k_pair_scan -> k_col_exact)
-  uint32_t n_dimer;       // cis-dimer leads listed by k_classify this step (DIMER_MEMBERS 3)
   // observable bookkeeping (the per-step counts are reduced by k_finalize)
   int32_t off_bond, off_rl, off_cis, off_mono;  // counters − derived at load
   int32_t maxc;                                 // protein_num_in_Max_Complex

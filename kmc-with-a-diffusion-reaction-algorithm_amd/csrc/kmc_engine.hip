@@ -21,13 +21,13 @@ using namespace kmcd;
 enum KId {
   KI_CLASSIFY, KI_BFS, KI_PROPOSE, KI_PROPOSE_FREE, KI_MOVE_MEMBERS, KI_CX_CHECK, KI_CX_HEAVY, KI_CX_KILL,
   KI_PAIR_SCAN, KI_COL_EXACT, KI_COL_ROUNDS, KI_COMMIT, KI_RXN_EXACT, KI_MATCH, KI_DISS_OBSERVE,
-  KI_RESORT, KI_PROPOSE_DIMER, KI_N
+  KI_RESORT, KI_N
 };
 static const char* const KNAMES[KI_N] = {
     "k_classify", "k_bfs", "k_propose", "k_propose_free", "k_move_members", "k_cx_check", "k_complex_heavy",
     "k_cx_kill",
     "k_pair_scan", "k_col_exact", "k_col_rounds", "k_commit", "k_rxn_exact",
-    "k_match", "k_diss_observe", "slot_resort", "k_propose_dimer"};
+    "k_match", "k_diss_observe", "slot_resort"};
 #define TRING 64  // steps of event pairs kept in flight
 
 struct kmc_sim {
@@ -41,7 +41,6 @@ struct kmc_sim {
   // end waits for it (REJ_SIDE)
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  hipEvent_t ev_dfork = nullptr, ev_djoin = nullptr;  // the cis dimers' moves beside the free units (DIMER_KERNEL 2)
   int64_t step_done = 0;
   std::string err;
   int ncell = 0;
@@ -248,9 +247,7 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&s->ev_dfork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&s->ev_djoin, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming) != hipSuccess) {
     kmc_destroy(s);
     return KMC_ERR_HIP;
   }
@@ -354,7 +351,6 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   rc |= dalloc(s, &d.overflow, NB);
   rc |= dalloc(s, &d.cx_list, (size_t)d.mcap / 2);  // kept across steps: every registration since the last rebuild
   rc |= dalloc(s, &d.cx_heavy, NB);
-  rc |= dalloc(s, &d.dimers, NA / 2 + 1);
   rc |= dalloc(s, &s->hcnt, s->ncell + 1);
   rc |= dalloc(s, &d.hstart, s->ncell + 1);
   rc |= dalloc(s, &d.home, N);
@@ -480,8 +476,6 @@ int kmc_destroy(kmc_sim* s) {
     if (g.exec) (void)hipGraphExecDestroy(g.exec);
   if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);
   if (s->ev_join) (void)hipEventDestroy(s->ev_join);
-  if (s->ev_dfork) (void)hipEventDestroy(s->ev_dfork);
-  if (s->ev_djoin) (void)hipEventDestroy(s->ev_djoin);
   if (s->side) (void)hipStreamDestroy(s->side);
   if (s->stream) (void)hipStreamDestroy(s->stream);
   delete s;
@@ -833,34 +827,9 @@ static int launch_step(kmc_sim* s, bool re_sort) {
       TIMED(KI_BFS, (k_bfs<<<gB, T, 0, st>>>(K, d)));
     }
     const int gC = K.NB > 0 ? std::min(gL, 512) : 0;  // grid-stride over the descriptor list
-    const int gA = std::max(1, (K.NA + T - 1) / T);
-#if DIMER_KERNEL == 2 || (DIMER_MEMBERS == 3 && DIMER_SIDE)
-    // the cis dimers on the side stream, beside the free units (both only
-    // read R and write their own proteins' R_new and records)
-    HIPCHK(s, hipEventRecord(s->ev_dfork, st));
-    HIPCHK(s, hipStreamWaitEvent(s->side, s->ev_dfork, 0));
-#if DIMER_KERNEL == 2
-    TIMED_ON(KI_PROPOSE_DIMER, s->side, (k_propose_dimer<<<gA, T, 0, s->side>>>(K, d)));
-#else
-    TIMED_ON(KI_PROPOSE_DIMER, s->side, (k_move_dimer_list<<<std::min(gA, 256), T, 0, s->side>>>(K, d)));
-#endif
-    HIPCHK(s, hipEventRecord(s->ev_djoin, s->side));
-#endif
     TIMED(KI_PROPOSE_FREE, (k_propose_free<<<gC + gN, T, 0, st>>>(K, d, gC)));
-#if DIMER_KERNEL == 1
-    TIMED(KI_PROPOSE_DIMER, (k_propose_dimer<<<gA, T, 0, st>>>(K, d)));
-#elif DIMER_KERNEL == 2 || (DIMER_MEMBERS == 3 && DIMER_SIDE)
-    HIPCHK(s, hipStreamWaitEvent(st, s->ev_djoin, 0));
-#endif
-    if (K.NB > 0 || DIMER_MEMBERS == 1) {  // (the cis dimers too, DIMER_MEMBERS 1)
-      TIMED(KI_MOVE_MEMBERS, (k_move_members<<<gN, T, 0, st>>>(K, d)));
-    }
-#if DIMER_MEMBERS == 2
-    TIMED(KI_PROPOSE_DIMER, (k_move_dimers<<<gA, T, 0, st>>>(K, d)));
-#elif DIMER_MEMBERS == 3 && !DIMER_SIDE
-    TIMED(KI_PROPOSE_DIMER, (k_move_dimer_list<<<std::min(gA, 256), T, 0, st>>>(K, d)));
-#endif
     if (K.NB > 0) {
+      TIMED(KI_MOVE_MEMBERS, (k_move_members<<<gN, T, 0, st>>>(K, d)));
       TIMED(KI_CX_CHECK, (k_cx_check<<<gL, T, 0, st>>>(K, d)));
       TIMED(KI_CX_HEAVY, (k_complex_heavy<<<1024, T, 0, st>>>(K, d)));
     }

@@ -70,7 +70,6 @@ struct Dev {
   uint32_t* pend;    // [N] round tag: unit still waiting (resolution pass C)
   int32_t* overflow; // [NB]
   int4* cx_list;     // [NB] descriptors of the registered complexes (kept across steps; cx_params, k_cx_check)
-  int32_t* dimers;   // [NA / 2 + 1] this step's cis-dimer leads (DIMER_MEMBERS 3)
   int4* cx_heavy;    // [NB] descriptors for k_complex_heavy: larger complexes, and those k_cx_check
                      //      moved but whose lay-down / alignment changes beads
   // Home list (§records): every protein has a home position hp in an order
@@ -194,21 +193,6 @@ __device__ __forceinline__ uint32_t wave_alloc(uint32_t* ctr, uint32_t qn) {
   return (uint32_t)__shfl((int)base, leader, 64) + pre;
 }
 
-// Where the cis dimers move (A/B builds): 0 the lead's thread in
-// k_propose_free (propose_dimer); DIMER_KERNEL 1 / 2 the lead's thread in a
-// kernel of its own after / beside it; DIMER_MEMBERS: each member's own thread
-// (move_dimer_member) — 1 in k_move_members, 2 in a sweep over the receptor
-// slots (k_move_dimers), 3 from a list k_classify compacts (k_move_dimer_list).
-#ifndef DIMER_KERNEL
-#define DIMER_KERNEL 0
-#endif
-#ifndef DIMER_MEMBERS
-#define DIMER_MEMBERS 0
-#endif
-#ifndef DIMER_SIDE  // DIMER_MEMBERS 3: the list kernel on a second stream beside k_propose_free
-#define DIMER_SIDE 0
-#endif
-
 // ================================================================ 1. classify
 // Unit kinds, main.cpp:584 (free receptor), 682-686 (cis dimer, moved at the
 // lower index), 905 (single ligand = BFS component of size 1).
@@ -229,9 +213,6 @@ __global__ void k_classify(KParams P, Dev d) {
       const bool lead = d.id_of[i] < d.id_of[q];  // moved at the lower reference index
       own = lead ? i : q;
       kind = lead ? U_DIMER : U_DIMER_P;
-#if DIMER_MEMBERS == 3
-      if (lead && d.croot[p] < 0) d.dimers[wave_slot(&d.ctl->n_dimer)] = p;
-#endif
     }
   } else {
     int b = p - NA;
@@ -672,84 +653,7 @@ __device__ __forceinline__ void put_recs_glb(const KParams& P, const Dev& d, int
 
 // free receptor, main.cpp:584-635.  All 48 coordinates are loaded (24 16-byte
 // rows) before the first store (R and R_new are distinct buffers), so a lane
-// has every load in flight at once.  FREE_HALF (A/B builds): two domains at a
-// time (12 rows in flight, fewer registers: one more wave per SIMD).
-#ifndef FREE_HALF
-#define FREE_HALF 0
-#endif
-#if FREE_HALF
-__device__ void propose_free_a(const KParams& P, const Dev& d, int i, uint32_t step) {
-  const uint2 h = d.home[i];
-  double u0, u1, u2, u3;
-  const uint32_t ri = (uint32_t)d.id_of[i];
-  kmcr::uniform2(P.key, kmcr::DOM_DIFF, ri, 0, step, 0, &u0, &u1);
-  kmcr::uniform2(P.key, kmcr::DOM_DIFF, ri, 0, step, 1, &u2, &u3);
-  double amp = P.amp_a * u0;
-  double phai = u1 * 2 * P.pai;
-  double dx = amp * kmcm::cos(phai), dy = amp * kmcm::sin(phai);
-  Rot t = euler(0, 0, (2 * u2 - 1) * P.rot_a);
-  double PBx = 0.0, PBy = 0.0;
-  double ocx[4], ocy[4], oz1[4], ncx[4], ncy[4], nz1[4], osx = 0.0, osy = 0.0, nsx = 0.0, nsy = 0.0;
-#pragma unroll
-  for (int hh = 0; hh < 2; ++hh) {
-    double2 v[12];  // (x, y) rows of domains 2hh+1, 2hh+2, then their z-pair rows
-#pragma unroll
-    for (int r = 0; r < 8; ++r) v[r] = ld_r(d.cur.A2(i, hh * 8 + r));
-#pragma unroll
-    for (int k = 0; k < 4; ++k) v[8 + k] = ld_r(d.cur.A2(i, 16 + hh * 4 + k));
-    if (hh == 0) {  // periodic shift from [1][1]
-      double o11x = v[0].x + dx, o11y = v[0].y + dy;
-      PBx = P.box_x * kmcm::round_(o11x / P.box_x);
-      PBy = P.box_y * kmcm::round_(o11y / P.box_y);
-    }
-    double nz[2][4];
-#pragma unroll
-    for (int jj = 0; jj < 2; ++jj) {
-      const int j = 2 * hh + jj;
-      const double cx = (v[jj * 4].x + dx) - PBx;
-      const double cy = (v[jj * 4].y + dy) - PBy;
-      const double cz = jj ? v[8].y : v[8].x;
-      ocx[j] = v[jj * 4].x;
-      ocy[j] = v[jj * 4].y;
-      oz1[j] = cz;
-      ncx[j] = cx;
-      ncy[j] = cy;
-      nz1[j] = cz;
-      nz[jj][0] = cz;
-      st_n(d.nxt.A2(i, j * 4), make_double2(cx, cy));
-#pragma unroll
-      for (int k = 1; k < 4; ++k) {
-        const double ox = (v[jj * 4 + k].x + dx) - PBx;
-        const double oy = (v[jj * 4 + k].y + dy) - PBy;
-        const double oz = jj ? v[8 + k].y : v[8 + k].x;
-        const double nx = rx(t, ox, oy, oz, cx, cy, cz), ny = ry(t, ox, oy, oz, cx, cy, cz);
-        st_n(d.nxt.A2(i, j * 4 + k), make_double2(nx, ny));
-        if (j == 2 && k == 2) {  // the [3][3] cis site (reaction prefilter)
-          osx = v[jj * 4 + k].x;
-          osy = v[jj * 4 + k].y;
-          nsx = nx;
-          nsy = ny;
-        }
-        nz[jj][k] = rz(t, ox, oy, oz, cx, cy, cz);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) st_n(d.nxt.A2(i, 16 + hh * 4 + k), make_double2(nz[0][k], nz[1][k]));
-  }
-  bool ext = true;
-#pragma unroll
-  for (int j = 1; j < 4; ++j) {
-    double ex = ncx[j] - ncx[0], ey = ncy[j] - ncy[0];
-    ext &= ex * ex + ey * ey <= 0.09;
-  }
-  if (!ext) atomicOr(&d.ctl->err, ERR_GEOMETRY);
-  const int own = (int)ri;  // a free receptor is its own unit, status bits 0
-  put_rec(P, d, h, i, 0, 0, own, ocx[0], ocy[0], fmin(fmin(oz1[0], oz1[1]), fmin(oz1[2], oz1[3])),
-          fmax(fmax(oz1[0], oz1[1]), fmax(oz1[2], oz1[3])), osx, osy);
-  put_rec(P, d, h, i, 1, 0, own, ncx[0], ncy[0], fmin(fmin(nz1[0], nz1[1]), fmin(nz1[2], nz1[3])),
-          fmax(fmax(nz1[0], nz1[1]), fmax(nz1[2], nz1[3])), nsx, nsy);
-}
-#else
+// has every load in flight at once.
 __device__ void propose_free_a(const KParams& P, const Dev& d, int i, uint32_t step) {
   double r[4][4][3];
 #pragma unroll
@@ -822,7 +726,6 @@ __device__ void propose_free_a(const KParams& P, const Dev& d, int i, uint32_t s
   put_rec(P, d, h, i, 1, 0, own, ncx[0], ncy[0], fmin(fmin(nz[0][0], nz[1][0]), fmin(nz[2][0], nz[3][0])),
           fmax(fmax(nz[0][0], nz[1][0]), fmax(nz[2][0], nz[3][0])), nsx, nsy);
 }
-#endif
 
 // snap receptor a2 onto a1's cis site (x,y of all 16 beads), main.cpp:786-798
 template <class S>
@@ -2163,125 +2066,6 @@ __device__ __forceinline__ void move_member(const KParams& P, const Dev& d, int 
   if (!ext) atomicOr(&d.cx_ext[root - P.NA], 1u);
 }
 
-// A cis dimer's member moved by its own thread (DIMER_MEMBERS, k_move_members),
-// main.cpp:682-865: each member draws the pair's move (the lead's keyed
-// draws), derives the shift and the centre from the [j][1] rows of both, and
-// moves its own 24 rows as a complex member does (the same expressions as
-// propose_dimer); the partner then applies the relax (main.cpp:770-799)
-// against the lead's new [3][1] and [3][3], which it computes from the lead's
-// old rows with the same move.  So the pair's rows stream like every other
-// protein's (coalesced, one thread each), and k_propose_free keeps no dimer
-// path (its registers: one more wave per SIMD).
-__device__ __forceinline__ void move_dimer_member(const KParams& P, const Dev& d, int p, bool lead) {
-  const int NA = P.NA;
-  const int o = A_NEI3(d, p) - 1, i = lead ? p : o, q = lead ? o : p;
-  const uint32_t step = d.ctl->step;
-  double u0, u1, u2, u3;
-  const uint32_t ri = (uint32_t)d.id_of[i];
-  kmcr::uniform2(P.key, kmcr::DOM_DIFF, ri, 0, step, 0, &u0, &u1);
-  kmcr::uniform2(P.key, kmcr::DOM_DIFF, ri, 0, step, 1, &u2, &u3);
-  const double amp = P.amp_cis * u0;
-  const double phai = u1 * 2 * P.pai;
-  const double dx = amp * kmcm::cos(phai), dy = amp * kmcm::sin(phai);
-  double cmx = 0, cmy = 0, cmz = 0, PBx, PBy;
-  double2 l31, l33;  // the lead's old [3][1], [3][3] (x, y) (partner: the relax)
-  double l31z, l33z;
-  {
-    double2 ci[4], cq[4], zi[2], zq[2];  // [j][1] (x, y); z of [1,2][1] and [3,4][1]
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      ci[j] = d.cur.A2(i, j * 4);
-      cq[j] = d.cur.A2(q, j * 4);
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      zi[h] = d.cur.A2(i, 16 + h * 4);
-      zq[h] = d.cur.A2(q, 16 + h * 4);
-    }
-    l31 = ci[2];
-    l31z = zi[1].x;
-    PBx = P.box_x * kmcm::round_(((ci[0].x + dx) + (cq[0].x + dx)) / 2 / P.box_x);
-    PBy = P.box_y * kmcm::round_(((ci[0].y + dy) + (cq[0].y + dy)) / 2 / P.box_y);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      cmx = cmx + ci[j].x + cq[j].x;
-      cmy = cmy + ci[j].y + cq[j].y;
-      cmz = cmz + (j & 1 ? zi[j >> 1].y : zi[j >> 1].x) + (j & 1 ? zq[j >> 1].y : zq[j >> 1].x);
-    }
-  }
-  if (!lead) {
-    l33 = d.cur.A2(i, 10);
-    l33z = d.cur.A2(i, 22).x;
-  }
-  cmx = cmx / (4 * 2);
-  cmy = cmy / (4 * 2);
-  cmz = cmz / (4 * 2);
-  const Rot t = euler(0, 0, (2 * u2 - 1) * P.rot_cis);
-  const double2* src = reinterpret_cast<const double2*>(d.cur.a);
-  double2* dst = reinterpret_cast<double2*>(d.nxt.a);
-  double2 r[ROWS_A];
-#pragma unroll
-  for (int w = 0; w < ROWS_A; ++w) r[w] = ld_r(src[bead_elem(p, w, NA, ROWS_A)]);
-  const uint2 h = d.home[p];
-  const int st = rec_status(P, d, p), own = d.owner[p];
-  put_rec(P, d, h, p, 0, st, own, r[0].x, r[0].y, fmin(fmin(r[16].x, r[16].y), fmin(r[20].x, r[20].y)),
-          fmax(fmax(r[16].x, r[16].y), fmax(r[20].x, r[20].y)), r[10].x, r[10].y);
-#pragma unroll
-  for (int jp = 0; jp < 2; ++jp)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int r1 = 2 * jp * 4 + k, r2 = (2 * jp + 1) * 4 + k, rzr = 16 + jp * 4 + k;
-      const double z1 = r[rzr].x, z2 = r[rzr].y;
-      const double ox1 = (r[r1].x + dx) - PBx, oy1 = (r[r1].y + dy) - PBy;
-      const double ox2 = (r[r2].x + dx) - PBx, oy2 = (r[r2].y + dy) - PBy;
-      r[r1] = make_double2(rx(t, ox1, oy1, z1, cmx, cmy, cmz), ry(t, ox1, oy1, z1, cmx, cmy, cmz));
-      r[r2] = make_double2(rx(t, ox2, oy2, z2, cmx, cmy, cmz), ry(t, ox2, oy2, z2, cmx, cmy, cmz));
-      r[rzr] = make_double2(rz(t, ox1, oy1, z1, cmx, cmy, cmz), rz(t, ox2, oy2, z2, cmx, cmy, cmz));
-    }
-  if (!lead) {
-    // relax, main.cpp:770-799: the lead's new [3][1], [3][3] against ours
-    double ox = (l31.x + dx) - PBx, oy = (l31.y + dy) - PBy;
-    const double2 n31 = make_double2(rx(t, ox, oy, l31z, cmx, cmy, cmz), ry(t, ox, oy, l31z, cmx, cmy, cmz));
-    ox = (l33.x + dx) - PBx;
-    oy = (l33.y + dy) - PBy;
-    const double2 n33 = make_double2(rx(t, ox, oy, l33z, cmx, cmy, cmz), ry(t, ox, oy, l33z, cmx, cmy, cmz));
-    double ex = n33.x - r[10].x, ey = n33.y - r[10].y;
-    const double dist2 = kmcm::sqrt_(ex * ex + ey * ey);
-    ex = n31.x - r[8].x;
-    ey = n31.y - r[8].y;
-    const double dist1 = kmcm::sqrt_(ex * ex + ey * ey);
-    if (!AreSame(dist1, P.cis_cut / 2 + P.ra + P.ra) || !AreSame(dist2, P.cis_cut / 2)) {
-      // snap onto the lead's cis site (main.cpp:786-798, snap_cis): every
-      // domain's beads 1 and 4 at (x1, y1), 3 at (x3, y3), 2 at (x2, y2)
-      const double RA = P.ra, cc = P.cis_cut;
-      const double x1 = (cc / 2 + RA) / RA * (n33.x - n31.x) + n33.x;
-      const double y1 = (cc / 2 + RA) / RA * (n33.y - n31.y) + n33.y;
-      const double x3 = (cc / 2) / RA * (n33.x - n31.x) + n33.x;
-      const double y3 = (cc / 2) / RA * (n33.y - n31.y) + n33.y;
-      const double x2 = (cc / 2 + 2 * RA) / RA * (n33.x - n31.x) + n33.x;
-      const double y2 = (cc / 2 + 2 * RA) / RA * (n33.y - n31.y) + n33.y;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        r[j * 4] = make_double2(x1, y1);
-        r[j * 4 + 1] = make_double2(x2, y2);
-        r[j * 4 + 2] = make_double2(x3, y3);
-        r[j * 4 + 3] = make_double2(x1, y1);
-      }
-    }
-  }
-#pragma unroll
-  for (int w = 0; w < ROWS_A; ++w) st_n(dst[bead_elem(p, w, NA, ROWS_A)], r[w]);
-  put_rec(P, d, h, p, 1, st, own, r[0].x, r[0].y, fmin(fmin(r[16].x, r[16].y), fmin(r[20].x, r[20].y)),
-          fmax(fmax(r[16].x, r[16].y), fmax(r[20].x, r[20].y)), r[10].x, r[10].y);
-  bool ext = true;
-#pragma unroll
-  for (int j = 1; j < 4; ++j) {
-    const double ex = r[j * 4].x - r[0].x, ey = r[j * 4].y - r[0].y;
-    ext &= ex * ex + ey * ey <= 0.09;
-  }
-  if (!ext) atomicOr(&d.ctl->err, ERR_GEOMETRY);
-}
-
 __global__ void __launch_bounds__(256) k_cx_check(KParams P, Dev d) {
   const int NA = P.NA, NB = P.NB;
   const uint32_t n = d.ctl->n_cx;
@@ -2319,9 +2103,6 @@ __global__ void __launch_bounds__(256) k_cx_check(KParams P, Dev d) {
 // move and the alignment on global memory.  Block 0's first wave first runs
 // the BFS of the components that overflowed k_bfs's LDS queue (> BFS_QCAP
 // members) and moves those it roots.  Launched after k_cx_check on its stream.
-#ifndef HEAVY_PREFETCH  // the next complex's descriptor and member records loaded during this one
-#define HEAVY_PREFETCH 0
-#endif
 #ifndef HEAVY_WAVES  // minimum waves per SIMD of k_complex_heavy (the register budget: 2 = 256, 3 = 168 VGPRs)
 #define HEAVY_WAVES 2
 #endif
@@ -2362,16 +2143,6 @@ __global__ void __launch_bounds__(256, HEAVY_WAVES) k_complex_heavy(KParams P, D
   }
   const uint32_t n = d.ctl->n_heavy;
   const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
-#if HEAVY_PREFETCH
-  // the wave's next complex: its descriptor is loaded when this one starts,
-  // its member records while this one is aligned, so a staged complex waits
-  // for one round trip (its beads) instead of three
-  int4 desc_n = w < n ? d.cx_heavy[w] : make_int4(0, 0, 0, 0);
-  auto mrec_of = [&](int4 dn) {
-    return (dn.x & CXD_MOVED) && lane < (dn.z & 0xffff) ? d.mrec[dn.y + lane] : make_int4(0, 0, 0, 0);
-  };
-  int4 mrec_n = w < n ? mrec_of(desc_n) : make_int4(0, 0, 0, 0);
-#endif
   for (uint32_t c = w; c < n; c += nw) {
 #ifdef KMC_STAMPS  // diagnostic build: per-phase cycles of the staged path (lane 0 of each wave)
     uint64_t t0_ = Stamper::now(), t_ = t0_;
@@ -2386,27 +2157,14 @@ __global__ void __launch_bounds__(256, HEAVY_WAVES) k_complex_heavy(KParams P, D
 #else
 #define CXS(i)
 #endif
-#if HEAVY_PREFETCH
-    const int4 desc = desc_n, mrec = mrec_n;
-    const bool more = c + nw < n;
-    if (more) desc_n = d.cx_heavy[c + nw];
-#else
     const int4 desc = d.cx_heavy[c];
-#endif
     const int lb = desc.x & CXD_LB;
     if (!(desc.x & CXD_MOVED)) {
       global_path(lb);
-#if HEAVY_PREFETCH
-      if (more) mrec_n = mrec_of(desc_n);
-#endif
       continue;
     }
     const int csize = desc.z & 0xffff, nB = desc.z >> 16;
-#if HEAVY_PREFETCH
-    const int mslot = cx_stage_mrec_r(L, mrec, csize, NA, lane);
-#else
     const int mslot = cx_stage_mrec(d, L, desc.y, csize, NA, lane);
-#endif
     // this lane's member's record inputs (cx_put_new), loaded here, long before use
     uint2 mhome = make_uint2(0u, 0u);
     int mst = 0;
@@ -2423,9 +2181,6 @@ __global__ void __launch_bounds__(256, HEAVY_WAVES) k_complex_heavy(KParams P, D
           L->rnd[call][pos] = kmcr::rand31(P.key, kmcr::DOM_SHUF, (uint32_t)desc.w, call, step, pos);
       }
     wave_sync();
-#if HEAVY_PREFETCH
-    if (more) mrec_n = mrec_of(desc_n);
-#endif
     CXS(0);
     {
       // the last receptor in member order: the highest lane holding one
@@ -2466,18 +2221,12 @@ __device__ __forceinline__ void propose_one(const KParams& P, const Dev& d, int 
   uint8_t k = d.ukind[p];
   if (k == U_FREE_A) {
     propose_free_a(P, d, p, step);
-  } else if (k == U_DIMER && !DIMER_KERNEL && !DIMER_MEMBERS) {
+  } else if (k == U_DIMER) {
     const int q = A_NEI3(d, p) - 1;
     propose_dimer(P, d, p, q, step);
   } else if (k == U_FREE_B) {
     propose_free_b(P, d, p - P.NA, p, step);
   }
-}
-
-__global__ void __launch_bounds__(256) k_propose_dimer(KParams P, Dev d) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x, NA = P.NA;
-  if (p >= NA || d.ukind[p] != U_DIMER) return;
-  propose_dimer(P, d, p, A_NEI3(d, p) - 1, d.ctl->step);
 }
 
 // member p of a complex of at most CXL members (cx_params), one thread per
@@ -2488,39 +2237,11 @@ __global__ void __launch_bounds__(256) k_propose_dimer(KParams P, Dev d) {
 __global__ void __launch_bounds__(256, MEMBER_WAVES) k_move_members(KParams P, Dev d) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x, NA = P.NA;
   if (p >= P.N) return;
-#if DIMER_MEMBERS == 1
-  if (p < NA) {
-    const uint8_t k = d.ukind[p];
-    if (k == U_DIMER || k == U_DIMER_P) {
-      move_dimer_member(P, d, p, k == U_DIMER);
-      return;
-    }
-  }
-#endif
   const int r = d.croot[p];
   if (r < 0 || d.cx_size[r - NA] > CXL) return;
   const double* cp = d.cxp + (size_t)(r - NA) * CXP;
   if (p < NA) move_member<true>(P, d, p, cp, r);
   else move_member<false>(P, d, p - NA, cp, r);
-}
-
-// the cis dimers' members from this step's list, one thread per member
-// (DIMER_MEMBERS 3): a small grid, so a wave is not held by one dimer's
-// dependent loads among 63 idle lanes of a sweep over every slot
-__global__ void __launch_bounds__(256) k_move_dimer_list(KParams P, Dev d) {
-  const uint32_t n = 2 * d.ctl->n_dimer;
-  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
-    const int lead = d.dimers[e >> 1], NA = P.NA;
-    move_dimer_member(P, d, (e & 1) ? A_NEI3(d, lead) - 1 : lead, !(e & 1));
-  }
-}
-
-// the cis dimers' members, one thread per receptor slot (DIMER_MEMBERS 2)
-__global__ void __launch_bounds__(256) k_move_dimers(KParams P, Dev d) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= P.NA) return;
-  const uint8_t k = d.ukind[p];
-  if (k == U_DIMER || k == U_DIMER_P) move_dimer_member(P, d, p, k == U_DIMER);
 }
 
 // the free units, one thread per slot
@@ -4377,7 +4098,6 @@ __global__ void __launch_bounds__(256) k_finalize(KParams P, Dev d, double time_
   c->n_cisc = 0;
   c->n_outl = 0;
   c->n_dense = 0;
-  c->n_dimer = 0;
 }
 
 
