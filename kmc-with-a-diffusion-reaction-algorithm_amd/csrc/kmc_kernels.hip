@@ -3591,6 +3591,9 @@ __device__ __forceinline__ bool pair_scan_block(const KParams& P, const Dev& d, 
 // stays free of that path's registers and call frame (measured: a fallback
 // inside costs it a third of its speed, through the lost occupancy or the
 // scratch frame).
+#ifndef PAIR_XCD  // tiles dealt to the XCDs in contiguous runs (A/B, profiles/r04/ab_r4w: the
+#define PAIR_XCD 1   // scan's HBM fetch 79 -> 37 MB per launch at C3, its time +1 us)
+#endif
 #ifndef PAIR_WAVES  // minimum waves per SIMD of the pair scan (A/B builds: tools/build_variants.py)
 #define PAIR_WAVES 5
 #endif
@@ -3600,13 +3603,22 @@ __global__ void __launch_bounds__(256, PAIR_WAVES) k_pair_scan(KParams P, Dev d)
   WgList& Lc = T.u.l.Lc;
   WgList& Lr = T.u.l.Lr;
   const int ntx = (P.ncx + P.tile - 1) / P.tile;
-  const int tx = blockIdx.x % ntx, ty = blockIdx.x / ntx;
+#if PAIR_XCD
+  // XCD-aware tile order: consecutive workgroups go to the 8 XCDs in turn, so
+  // workgroup b takes tile k = b / 8 of XCD b % 8's contiguous run of tiles —
+  // neighbouring tiles, which stage each other's halo records, share an L2
+  const int nt = (int)gridDim.x, q8 = nt / 8, r8 = nt % 8, xcd = (int)blockIdx.x % 8;
+  const int tile = xcd * q8 + min(xcd, r8) + (int)blockIdx.x / 8;
+#else
+  const int tile = (int)blockIdx.x;
+#endif
+  const int tx = tile % ntx, ty = tile / ntx;
   const int x0 = tx * P.tile, y0 = ty * P.tile, w = min(P.tile, P.ncx - x0), h = min(P.tile, P.ncy - y0);
   if (threadIdx.x == 0) {  // this tile's outlier bucket (read before tile_load's first barrier), then reset
-    const uint32_t no = d.tout_n[blockIdx.x];
+    const uint32_t no = d.tout_n[tile];
     T.nout = no;
-    T.obkt = no <= (uint32_t)P.tout_cap ? (int)blockIdx.x : -1;
-    if (no) d.tout_n[blockIdx.x] = 0;
+    T.obkt = no <= (uint32_t)P.tout_cap ? tile : -1;
+    if (no) d.tout_n[tile] = 0;
   }
   Stamper S(0);
   if (!pair_scan_block(P, d, tile_geo(x0, y0, w, h), T, site, Lc, Lr, S) && threadIdx.x == 0) {
