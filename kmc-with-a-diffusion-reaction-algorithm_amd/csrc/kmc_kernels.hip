@@ -3384,13 +3384,13 @@ __device__ __forceinline__ void rej_copy(const KParams& P, const Dev& d, int m, 
   dst[e] = src[e];
 }
 
-// One group of REJ_LANES lanes per rejected unit (four units per wave); its
+// One group of REJ_LANES lanes per rejected unit (two units per wave); its
 // lanes take the (member, bead row) copies of all members at once, so a
 // complex costs the same few dependent loads as a single protein, and a wave
 // carries four units' dependent chains at once (most rejected units are
 // single proteins of 12 or 24 rows).
-#ifndef REJ_LANES
-#define REJ_LANES 16
+#ifndef REJ_LANES  // (A/B, profiles/r04/ab_r4x: 16 -> 32 lanes, k_rej_commit 21.2 -> 18.4 us at C3)
+#define REJ_LANES 32
 #endif
 #ifndef REJ_SIDE  // k_rej_commit on a second stream beside k_rxn_exact .. k_finalize (kmc_engine.hip)
 #define REJ_SIDE 0
