@@ -868,7 +868,7 @@ static int launch_step(kmc_sim* s, bool re_sort) {
   }
   TIMED(KI_DISS_OBSERVE, {
     k_diss_observe<<<gN, T, 0, st>>>(K, d);
-    k_finalize<<<1, 256, 0, st>>>(K, d, s->p.time_step, gN);
+    k_finalize<<<1, 1024, 0, st>>>(K, d, s->p.time_step, gN);
   });
 #if REJ_SIDE
   HIPCHK(s, hipStreamWaitEvent(st, s->ev_join, 0));  // join: the next step reads R

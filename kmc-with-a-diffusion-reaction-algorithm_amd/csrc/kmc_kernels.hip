@@ -4031,14 +4031,16 @@ __global__ void __launch_bounds__(256) k_diss_observe(KParams P, Dev d) {
 }
 
 // bond.dat record (main.cpp:2195-2202, 2251) and step advance; one
-// workgroup reduces the observable partials of k_diss_observe's nblk blocks.
-// The list shard counters are totalled (diagnostics) and zeroed in parallel;
-// the control block is read in one batch of loads and written once.
-__global__ void __launch_bounds__(256) k_finalize(KParams P, Dev d, double time_step, int nblk) {
-  __shared__ int red[4][6];
+// workgroup of 1024 threads reduces the observable partials of
+// k_diss_observe's nblk blocks (39 063 at C5), four partials in flight per
+// thread.  The list shard counters are totalled (diagnostics) and zeroed in
+// parallel; the control block is read in one batch of loads and written once.
+__global__ void __launch_bounds__(1024) k_finalize(KParams P, Dev d, double time_step, int nblk) {
+  __shared__ int red[16][6];
   __shared__ uint32_t tot[5];
   if (threadIdx.x < 5) tot[threadIdx.x] = 0;
   int v[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll 4
   for (int b = threadIdx.x; b < nblk; b += blockDim.x) {
     const int4 lo = *(const int4*)&d.obs_part[b * 8];
     const int2 hi = *(const int2*)&d.obs_part[b * 8 + 4];
