@@ -3816,8 +3816,11 @@ struct CisV {
 // edges accepted before it, instead of the sort and dependency rounds of
 // block_greedy, whose barriers dominate at this size.
 #define SMALL_EDGES 64
+// Wave 0 returns its lane's sorted key and acceptance (the callers apply the
+// accepted edges from registers, without reading acc / keys back).
 template <typename VF>
-__device__ void small_greedy(uint32_t n, uint64_t* keys, VF vtx, uint8_t* acc) {
+__device__ bool small_greedy(uint32_t n, uint64_t* keys, VF vtx, uint8_t* acc, uint64_t* key_out) {
+  bool mine = false;
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     uint64_t k = lane < (int)n ? keys[lane] : ~0ull;
@@ -3838,9 +3841,12 @@ __device__ void small_greedy(uint32_t n, uint64_t* keys, VF vtx, uint8_t* acc) {
       const bool shares = (va == a) | (va == b) | (vb == a) | (vb == b);
       if ((__ballot(shares) & accm) == 0) accm |= 1ull << e;
     }
-    if (real) acc[lane] = (uint8_t)((accm >> lane) & 1ull);
+    mine = real && ((accm >> lane) & 1ull);
+    if (real) acc[lane] = (uint8_t)mine;
+    *key_out = k;
   }
   __syncthreads();
+  return mine;
 }
 
 // R–L association, main.cpp:1877-1949
@@ -3850,18 +3856,7 @@ __device__ void rl_match(const KParams& P, const Dev& d) {
   if (n == 0) return;
   if (n > d.cap_edges) n = d.cap_edges;
   uint8_t* acc = (uint8_t*)(d.gi32 + 5 * d.cap_edges);
-  if (n <= SMALL_EDGES) {
-    small_greedy(n, d.rl_keys, RLV{P.N}, acc);
-  } else {
-    uint32_t np = pow2ceil(n);
-    for (uint32_t e = n + threadIdx.x; e < np; e += blockDim.x) d.rl_keys[e] = ~0ull;
-    __syncthreads();
-    block_sort(d.rl_keys, np);
-    block_greedy(n, d.rl_keys, RLV{P.N}, d.ent, d.gi32, acc, &d.ctl->err);
-  }
-  for (uint32_t e = threadIdx.x; e < n; e += blockDim.x) {
-    if (!acc[e]) continue;
-    uint64_t key = d.rl_keys[e];
+  auto apply = [&](uint64_t key) {
     int i = d.slot_of[(int)(key >> 34)], q = d.slot_of[(int)((key >> 2) & 0xffffffffu)], k = (int)(key & 3) + 2;
     int lb = q - NA;
     A_ST2(d, i) = 1;
@@ -3871,7 +3866,19 @@ __device__ void rl_match(const KParams& P, const Dev& d) {
     A_NEI4(d, i) = k;
     mark_bond_change(P, d, i, d.ctl->step);
     mark_bond_change(P, d, q, d.ctl->step);
+  };
+  if (n <= SMALL_EDGES) {
+    uint64_t key = 0;
+    if (small_greedy(n, d.rl_keys, RLV{P.N}, acc, &key)) apply(key);
+    return;
   }
+  uint32_t np = pow2ceil(n);
+  for (uint32_t e = n + threadIdx.x; e < np; e += blockDim.x) d.rl_keys[e] = ~0ull;
+  __syncthreads();
+  block_sort(d.rl_keys, np);
+  block_greedy(n, d.rl_keys, RLV{P.N}, d.ent, d.gi32, acc, &d.ctl->err);
+  for (uint32_t e = threadIdx.x; e < n; e += blockDim.x)
+    if (acc[e]) apply(d.rl_keys[e]);
 }
 
 // cis association: mono (main.cpp:1952-2003) then complex (2007-2058)
@@ -3898,26 +3905,26 @@ __device__ void cis_match(const KParams& P, const Dev& d) {
     }
     __syncthreads();
     uint32_t n = m;
-    if (n > 0) {
-      if (n <= SMALL_EDGES) {
-        small_greedy(n, e, CisV{}, acc);
-      } else {
-        uint32_t np = pow2ceil(n);
-        for (uint32_t t = n + threadIdx.x; t < np; t += blockDim.x) e[t] = ~0ull;
-        __syncthreads();
-        block_sort(e, np);
-        block_greedy(n, e, CisV{}, d.ent, d.gi32, acc, &d.ctl->err);
-      }
-      for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) {
-        if (!acc[t]) continue;
-        int i = d.slot_of[(int)(e[t] >> 34)], q = d.slot_of[(int)((e[t] >> 2) & 0xffffffffu)];
-        A_ST3(d, i) = 1;
-        A_ST3(d, q) = 1;
-        A_NEI3(d, q) = i + 1;
-        A_NEI3(d, i) = q + 1;
-        mark_bond_change(P, d, i, d.ctl->step);
-        mark_bond_change(P, d, q, d.ctl->step);
-      }
+    auto apply = [&](uint64_t key) {
+      int i = d.slot_of[(int)(key >> 34)], q = d.slot_of[(int)((key >> 2) & 0xffffffffu)];
+      A_ST3(d, i) = 1;
+      A_ST3(d, q) = 1;
+      A_NEI3(d, q) = i + 1;
+      A_NEI3(d, i) = q + 1;
+      mark_bond_change(P, d, i, d.ctl->step);
+      mark_bond_change(P, d, q, d.ctl->step);
+    };
+    if (n > 0 && n <= SMALL_EDGES) {
+      uint64_t key = 0;
+      if (small_greedy(n, e, CisV{}, acc, &key)) apply(key);
+    } else if (n > 0) {
+      uint32_t np = pow2ceil(n);
+      for (uint32_t t = n + threadIdx.x; t < np; t += blockDim.x) e[t] = ~0ull;
+      __syncthreads();
+      block_sort(e, np);
+      block_greedy(n, e, CisV{}, d.ent, d.gi32, acc, &d.ctl->err);
+      for (uint32_t t = threadIdx.x; t < n; t += blockDim.x)
+        if (acc[t]) apply(e[t]);
     }
     __syncthreads();
   }
