@@ -141,8 +141,15 @@ def shared_device() -> bool:
     """KMC_BENCH_SHARED_DEVICE=1 (tests only): every rank on device 0 and the
     gloo backend, so the N-rank path (launcher, rendezvous, max over ranks,
     ensemble reduction) runs on a one-GPU box (tests/test_gpu_bench_ranks.py).
-    The line then says so in ensemble_reduce.shared_device."""
-    return os.environ.get("KMC_BENCH_SHARED_DEVICE") == "1"
+    Refused outside a pytest run (PYTEST_CURRENT_TEST): N ranks sharing one
+    GPU are not an N-GPU measurement.  The line then carries "value": null,
+    "shared_device": true and the one-device rate as "value_shared_device"."""
+    if os.environ.get("KMC_BENCH_SHARED_DEVICE") != "1":
+        return False
+    if not os.environ.get("PYTEST_CURRENT_TEST"):
+        sys.exit("bench.py: KMC_BENCH_SHARED_DEVICE=1 is a test-only mode (every rank on one GPU); "
+                 "refusing to report it as a measurement")
+    return True
 
 
 def launch(args, argv) -> int:
@@ -353,9 +360,10 @@ def run_rank(args, rank: int, world: int, local: int):
               file=sys.stderr)
 
     if rank == 0:
+        rate = world * n * args.steps / dt
         line = {
             "metric": METRIC,
-            "value": world * n * args.steps / dt,
+            "value": None if shared else rate,
             "unit": "particle-updates/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -405,6 +413,10 @@ def run_rank(args, rank: int, world: int, local: int):
             "ensemble_reduce": reduce_info,
             "library": library,
         }
+        if shared:
+            # every rank on one device (test mode): not an N-GPU throughput
+            line["shared_device"] = True
+            line["value_shared_device"] = rate
         os.write(json_fd, (json.dumps(line) + "\n").encode())
     sim.close()
     dist.destroy_process_group()

@@ -189,6 +189,39 @@ int kmc_host_append_cluster_log(const kmc_params* p, int64_t step, const int32_t
 /* bond-link consistency + rigid-body extent bound; KMC_OK or an error code */
 int kmc_host_validate(const kmc_params* p, const kmc_state_view* v);
 
+/* Domain decomposition of ONE trajectory over several handles (SURVEY.md
+ * §8(f).4; the host driver is slabs.py).  The reference has no
+ * counterpart: its step is one sequential loop (main.cpp:577, 1877-2058).
+ * A handle created for the n_a + n_b proteins of one slab's window (the
+ * proteins its slab owns plus halo copies of its neighbours') simulates the
+ * window with the trajectory's own random streams:
+ *   kmc_dd_set_state  the window in local numbering (receptors, then ligands,
+ *                     each increasing in the global index gid[]: every order
+ *                     the step takes is then the global one), own[i] = 1 for
+ *                     the proteins this slab owns (the observables count only
+ *                     those; a cis pair at its lower-index member), ctl5 =
+ *                     the counters' offsets (bond, rl, cis, mono_cis) and the
+ *                     running largest complex of this slab's share.
+ *   kmc_dd_export     the end-of-step state of local proteins ids[0..n):
+ *                     beads[n][48] (kmc_state_view bead order; a ligand uses
+ *                     the first 24) and ints[n][8] (receptor st2 st3 nei2
+ *                     nei4 nei3, ligand st1..4 nei1..4; links = local index+1).
+ *   kmc_dd_import     the owners' end-of-step state of halo proteins, same
+ *                     layout; flags[i] |= 1 where a coordinate differed from
+ *                     this handle's own result, 2 where a status / link did.
+ *   kmc_dd_drift      the largest periodic x displacement of an owned
+ *                     protein since kmc_dd_set_state.
+ *   kmc_dd_counters   out[0] collisions between an owned and a halo unit,
+ *                     out[1] bonds formed between an owned and a halo protein,
+ *                     both since kmc_dd_set_state. */
+int kmc_dd_set_state(kmc_sim* s, const kmc_state_view* v, const int32_t* gid, const uint8_t* own,
+                     const int32_t* ctl5);
+int kmc_dd_export(kmc_sim* s, int32_t n, const int32_t* ids, double* beads, int32_t* ints);
+int kmc_dd_import(kmc_sim* s, int32_t n, const int32_t* ids, const double* beads, const int32_t* ints,
+                  uint8_t* flags);
+int kmc_dd_drift(kmc_sim* s, double* max_dx);
+int kmc_dd_counters(kmc_sim* s, int64_t* out);
+
 /* Diagnostics: the portable math of kmc_math.h evaluated on the host and on
  * the device (op 0 sin, 1 cos, 2 atan2(x,y), 3 acos, 4 sqrt, 5 x/y, 6 round)
  * — the GPU numerics test compares the two bit for bit. */

@@ -38,6 +38,9 @@ struct KParams {
   int htag_max;   // tile home entries tagged for the direct lookup (<= HTAG_MAX; lowered only by KMC_DEBUG_HTAG)
   int dbg_recs;   // debug (KMC_DEBUG_RECS=1): every record stamped with its step and checked before the pair scan
   int dbg_cand;   // diagnostics (KMC_DEBUG_CAND=1): candidate / reaction-pair outcome counts (Ctl::cand_kind)
+  int dd;         // 1: this handle simulates one slab's window of a decomposed trajectory (kmc_dd_set_state):
+                  // random streams keyed by the global reference index (Dev::gid), observables over the
+                  // proteins this slab owns (Dev::dd_own); 0: the whole trajectory
 };
 
 // per-step control block in device memory (replayable without host writes)
@@ -74,6 +77,9 @@ struct Ctl {
                           // first distance gate, accepting
   uint64_t vtag;          // BFS tag counter for the overflow path
   uint64_t stamps[24];    // diagnostic build (-DKMC_STAMPS) only: phase cycles (tile scans, complexes)
+  // decomposed trajectories (KParams::dd), since kmc_dd_set_state: collisions found between a unit this
+  // slab owns and a unit it holds as a halo copy; bonds formed between an owned and a halo protein
+  uint32_t dd_xcol, dd_xbond;
 };
 
 enum : uint32_t {

@@ -36,11 +36,6 @@ struct kmc_sim {
   Dev d;
   int device = 0;
   hipStream_t stream = nullptr;
-  // the rejected units' R -> R_new revert runs on a second stream beside the
-  // reaction / observable kernels (neither reads what it writes); the step's
-  // end waits for it (REJ_SIDE)
-  hipStream_t side = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int64_t step_done = 0;
   std::string err;
   int ncell = 0;
@@ -108,6 +103,17 @@ struct kmc_sim {
   } graphs[NGRAPH];
   int graph_next = 0;
   int64_t graph_launches = 0, graph_captures = 0;
+  // one slab's window of a decomposed trajectory (kmc_dd_*): device copies of
+  // the local -> global index map, the ownership flags, x at the window's set
+  int32_t* dd_gid = nullptr;
+  uint8_t* dd_own = nullptr;
+  double* dd_x0 = nullptr;
+  uint32_t* dd_scratch = nullptr;  // [2]: drift maximum (float bits), differing proteins
+  int32_t* dd_ids = nullptr;       // export / import staging: ids, beads, ints, flags
+  double* dd_beads = nullptr;
+  int32_t* dd_ints = nullptr;
+  uint8_t* dd_flags = nullptr;
+  int32_t dd_cap = 0;
 };
 
 namespace {
@@ -244,10 +250,7 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
     delete s;
     return KMC_ERR_NODEVICE;
   }
-  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
     kmc_destroy(s);
     return KMC_ERR_HIP;
   }
@@ -474,9 +477,6 @@ int kmc_destroy(kmc_sim* s) {
     if (e) (void)hipEventDestroy(e);
   for (auto& g : s->graphs)
     if (g.exec) (void)hipGraphExecDestroy(g.exec);
-  if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);
-  if (s->ev_join) (void)hipEventDestroy(s->ev_join);
-  if (s->side) (void)hipStreamDestroy(s->side);
   if (s->stream) (void)hipStreamDestroy(s->stream);
   delete s;
   return KMC_OK;
@@ -611,8 +611,15 @@ static int snapshot(kmc_sim* s, bool restore) {
   return rc != KMC_OK ? rc : home_build(s);
 }
 
+static int set_state_impl(kmc_sim* s, const kmc_state_view* v);
+
 int kmc_set_state(kmc_sim* s, const kmc_state_view* v) {
   if (!s || !v) return KMC_ERR_ARG;
+  s->K.dd = 0;  // the whole trajectory (kmc_dd_set_state: one slab's window)
+  return set_state_impl(s, v);
+}
+
+static int set_state_impl(kmc_sim* s, const kmc_state_view* v) {
   int rc = kmch_host::validate(&s->p, v, &s->err);
   if (rc != KMC_OK) return rc;
   const int NA = s->p.n_a, NB = s->p.n_b;
@@ -781,11 +788,6 @@ struct Bracket {
     Bracket b_(s, k, s->stream); \
     __VA_ARGS__;                 \
   } while (0)
-#define TIMED_ON(k, stream, ...) \
-  do {                           \
-    Bracket b_(s, k, stream);    \
-    __VA_ARGS__;                 \
-  } while (0)
 
 // s->tnow (this step bracketed) is set by the caller
 static int launch_step(kmc_sim* s, bool re_sort) {
@@ -852,16 +854,10 @@ static int launch_step(kmc_sim* s, bool re_sort) {
     k_col_units<<<gX, T, 0, st>>>(K, d, 0);
     k_col_tail<<<1, 1024, 0, st>>>(K, d, 1);
   });
-#if REJ_SIDE
-  // fork: the revert on the side stream (k_rxn_exact reads each protein's
-  // final position from R or R_new by its record, not the reverted R_new)
-  HIPCHK(s, hipEventRecord(s->ev_fork, st));
-  HIPCHK(s, hipStreamWaitEvent(s->side, s->ev_fork, 0));
-  TIMED_ON(KI_COMMIT, s->side, (k_rej_commit<<<gX, T, 0, s->side>>>(K, d)));
-  HIPCHK(s, hipEventRecord(s->ev_join, s->side));
-#else
+  // (the revert cannot run beside the reactions: an association snaps the
+  // receptor in R_new, and a receptor of a rejected unit must be reverted
+  // before that — DESIGN.md §8, the rejected REJ_SIDE variant)
   TIMED(KI_COMMIT, (k_rej_commit<<<gX, T, 0, st>>>(K, d)));
-#endif
   if (K.NA > 0) {
     TIMED(KI_RXN_EXACT, (k_rxn_exact<<<1024, T, 0, st>>>(K, d)));
     TIMED(KI_MATCH, (k_match<<<1, 1024, 0, st>>>(K, d)));
@@ -870,9 +866,6 @@ static int launch_step(kmc_sim* s, bool re_sort) {
     k_diss_observe<<<gN, T, 0, st>>>(K, d);
     k_finalize<<<1, 1024, 0, st>>>(K, d, s->p.time_step, gN);
   });
-#if REJ_SIDE
-  HIPCHK(s, hipStreamWaitEvent(st, s->ev_join, 0));  // join: the next step reads R
-#endif
   if (s->tnow) s->tslot = (s->tslot + 1) % TRING;
   // R_new becomes R (main.cpp:2164-2191): swap the bead buffers
   std::swap(d.cur, d.nxt);
@@ -918,16 +911,18 @@ static int launch_step_graph(kmc_sim* s) {
   return KMC_OK;
 }
 
-// Launch n steps from the current state; device obs records land in obs_buf.
-// Returns after the stream has drained, with the control block in ctl_host.
-static int run_chunk(kmc_sim* s, int64_t n) {
+// Launch n steps from the current state, whose last completed step is `base`
+// (s->step_done, or an earlier step while replaying from the snapshot);
+// device obs records land in obs_buf.  Returns after the stream has drained,
+// with the control block in ctl_host.
+static int run_chunk(kmc_sim* s, int64_t n, int64_t base) {
   uint32_t zero = 0;
   HIPCHK(s, hipMemcpyAsync(&s->d.ctl->obs_idx, &zero, sizeof zero, hipMemcpyHostToDevice, s->stream));
   for (int64_t k = 0; k < n; ++k) {
     const bool rs = s->resort_every > 0 && ++s->since_resort >= s->resort_every;
     if (rs) s->since_resort = 0;
     // unit-state tags are (step mod 2^30): clear them when the tag wraps
-    if (((s->step_done + k + 1) & 0x3fffffff) == 0)
+    if (((base + k + 1) & 0x3fffffff) == 0)
       HIPCHK(s, hipMemsetAsync(s->d.ustate, 0, sizeof(uint32_t) * (size_t)s->K.N, s->stream));
     s->tnow = s->tmask && (s->tcount++ % s->tperiod) == 0;
     // graph replay for the plain steps: no re-sort, no full complex rebuild, no
@@ -981,7 +976,7 @@ int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out) {
       ++s->n_snapshots;
     }
     for (;;) {
-      rc = run_chunk(s, n);
+      rc = run_chunk(s, n, s->step_done);
       if (rc != KMC_OK) return rc;
       const uint32_t err = s->ctl_host->err;
       if (!err) break;
@@ -1006,11 +1001,28 @@ int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out) {
       }
       for (int64_t at = s->snap_step; at < s->step_done;) {
         const int64_t m = std::min(chunk, s->step_done - at);
-        rc = run_chunk(s, m);
+        rc = run_chunk(s, m, at);
         if (rc != KMC_OK) return rc;
         if (s->ctl_host->err) {
-          s->snap_valid = false;
-          return fail(s, KMC_ERR_HIP, "replay from the snapshot raised an error the original steps did not");
+          // the device is somewhere between the snapshot and step_done: go
+          // back to the snapshot (still valid) and say so — the host's step
+          // count must describe the device state
+          rc = snapshot(s, true);
+          if (rc != KMC_OK) {
+            s->have_state = false;  // neither state is known: the caller must set one
+            return rc;
+          }
+          const int64_t at_fail = at;
+          s->step_done = s->snap_step;
+          s->since_resort = s->snap_since;
+          s->need_full = true;
+          s->clusters_valid = false;
+          char m2[200];
+          snprintf(m2, sizeof m2,
+                   "replay from the snapshot raised an error the original steps did not (in steps %lld..%lld); "
+                   "state restored to step %lld",
+                   (long long)at_fail + 1, (long long)(at_fail + m), (long long)s->step_done);
+          return fail(s, KMC_ERR_HIP, m2);
         }
         at += m;
       }
@@ -1018,7 +1030,7 @@ int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out) {
       // keep the steps before the failing one
       const int64_t good = std::max<int64_t>(0, std::min<int64_t>(n, bad - (s->step_done + 1)));
       if (good > 0) {
-        rc = run_chunk(s, good);
+        rc = run_chunk(s, good, s->step_done);
         if (rc != KMC_OK) return rc;
         if (out)
           HIPCHK(s, hipMemcpy(out + done, s->obs_buf, sizeof(kmc_obs_dev) * good, hipMemcpyDeviceToHost));
@@ -1182,5 +1194,239 @@ int kmc_kernel_times(const kmc_sim* s, double* total_ms, int64_t* launches, int3
 }
 
 const char* kmc_kernel_name(int32_t id) { return id >= 0 && id < KI_N ? KNAMES[id] : ""; }
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- decomposed trajectory
+// One slab's window of a trajectory split over several handles (SURVEY.md
+// §8(f).4): the host driver (slabs.py) sets the window's
+// proteins with their global indices and ownership, steps every handle, and
+// moves the end-of-step state of each slab's boundary proteins to the
+// handles that hold them as halo copies.  Exchanged record of one protein:
+// 48 doubles (the kmc_state_view bead order: receptor ((j-1)·4 + k-1)·3 + c,
+// ligand ((j-1)·2 + k-1)·3 + c in the first 24) and 8 ints (receptor st2 st3
+// nei2 nei4 nei3, ligand st1..4 nei1..4; protein links are local reference
+// index + 1, 0 = none).
+__global__ void k_dd_export(KParams P, Dev d, int n, const int32_t* ids, double* beads, int32_t* ints) {
+  const int NA = P.NA, NB = P.NB;
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < (size_t)n * 48) {
+    const int i = (int)(t / 48), e = (int)(t % 48), slot = d.slot_of[ids[i]], bead = e / 3, c = e % 3;
+    double v = 0.0;
+    if (slot < NA) v = d.cur.A(slot, bead / 4 + 1, bead % 4 + 1, c);
+    else if (e < 24) v = d.cur.B(slot - NA, bead / 2 + 1, bead % 2 + 1, c);
+    beads[t] = v;
+  }
+  if (t < (size_t)n * 8) {
+    const int i = (int)(t / 8), f = (int)(t % 8), slot = d.slot_of[ids[i]];
+    int v = 0;
+    bool link = false;
+    if (slot < NA) {
+      if (f < 5) v = d.a_int[(size_t)f * NA + slot];
+      link = f == 2 || f == 4;
+    } else {
+      v = d.b_int[(size_t)f * NB + (slot - NA)];
+      link = f >= 4;
+    }
+    if (link && v > 0) v = d.id_of[v - 1] + 1;
+    ints[t] = v;
+  }
+}
+
+// The owner's end-of-step state of halo proteins into R and the state rows;
+// flags[i] |= 1 where a coordinate differed bit for bit from this handle's
+// own result, 2 where a status or link did.
+__global__ void k_dd_import(KParams P, Dev d, int n, const int32_t* ids, const double* beads, const int32_t* ints,
+                            uint8_t* flags) {
+  const int NA = P.NA, NB = P.NB;
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < (size_t)n * 48) {
+    const int i = (int)(t / 48), e = (int)(t % 48), slot = d.slot_of[ids[i]], bead = e / 3, c = e % 3;
+    double* dst = nullptr;
+    if (slot < NA) dst = &d.cur.A(slot, bead / 4 + 1, bead % 4 + 1, c);
+    else if (e < 24) dst = &d.cur.B(slot - NA, bead / 2 + 1, bead % 2 + 1, c);
+    if (dst) {
+      const double v = beads[t];
+      if (__double_as_longlong(*dst) != __double_as_longlong(v)) {
+        atomicOr((uint32_t*)&flags[i & ~3], 1u << (8 * (i & 3)));
+        *dst = v;
+      }
+    }
+  }
+  if (t < (size_t)n * 8) {
+    const int i = (int)(t / 8), f = (int)(t % 8), slot = d.slot_of[ids[i]];
+    int32_t* dst = nullptr;
+    bool link = false;
+    if (slot < NA) {
+      if (f < 5) dst = &d.a_int[(size_t)f * NA + slot];
+      link = f == 2 || f == 4;
+    } else {
+      dst = &d.b_int[(size_t)f * NB + (slot - NA)];
+      link = f >= 4;
+    }
+    if (dst) {
+      int v = ints[t];
+      if (link && v > 0) v = d.slot_of[v - 1] + 1;
+      if (*dst != v) {
+        atomicOr((uint32_t*)&flags[i & ~3], 2u << (8 * (i & 3)));
+        *dst = v;
+      }
+    }
+  }
+}
+
+// largest |x − x0| (periodic in x) of [1][1] over the proteins this slab owns
+__global__ void k_dd_drift(KParams P, Dev d, uint32_t* out) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  float m = 0.0f;
+  if (p < P.N) {
+    const int r = d.id_of[p];
+    if (d.dd_own[r]) {
+      double dx = d.cur.P(p, 1, 1, 0) - d.dd_x0[r];
+      dx = dx - P.box_x * kmcm::round_(dx / P.box_x);
+      m = (float)kmcm::fabs_(dx);
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_down(m, o, 64));
+  if (__lane_id() == 0) atomicMax(out, __float_as_uint(m));
+}
+
+extern "C" {
+
+static int dd_stage(kmc_sim* s, int32_t n) {
+  if (n <= s->dd_cap) return KMC_OK;
+  dfree(s, s->dd_ids);
+  dfree(s, s->dd_beads);
+  dfree(s, s->dd_ints);
+  dfree(s, s->dd_flags);
+  s->dd_cap = std::max<int32_t>(n, 1024);
+  int rc = dalloc(s, &s->dd_ids, (size_t)s->dd_cap);
+  rc |= dalloc(s, &s->dd_beads, (size_t)s->dd_cap * 48);
+  rc |= dalloc(s, &s->dd_ints, (size_t)s->dd_cap * 8);
+  rc |= dalloc(s, &s->dd_flags, ((size_t)s->dd_cap + 3) & ~(size_t)3);
+  return rc == KMC_OK ? KMC_OK : fail(s, KMC_ERR_HIP, "dd staging buffers");
+}
+
+int kmc_dd_set_state(kmc_sim* s, const kmc_state_view* v, const int32_t* gid, const uint8_t* own,
+                     const int32_t* ctl5) {
+  if (!s || !v || !gid || !own || !ctl5) return KMC_ERR_ARG;
+  const int NA = s->p.n_a, NB = s->p.n_b, N = NA + NB;
+  // the local numbering must be monotone in the global one (receptors, then
+  // ligands): every order the step takes (unit keys, BFS roots, the greedy
+  // reactions) then equals the global order restricted to the window
+  for (int i = 1; i < N; ++i)
+    if (gid[i] <= gid[i - 1]) return fail(s, KMC_ERR_ARG, "dd: global indices not increasing");
+  if (N > 0 && gid[0] < 0) return fail(s, KMC_ERR_ARG, "dd: negative global index");
+  if (!s->dd_gid) {
+    int rc = dalloc(s, &s->dd_gid, (size_t)N);
+    rc |= dalloc(s, &s->dd_own, (size_t)N);
+    rc |= dalloc(s, &s->dd_x0, (size_t)N);
+    rc |= dalloc(s, &s->dd_scratch, 2);
+    if (rc != KMC_OK) return fail(s, KMC_ERR_HIP, "dd buffers");
+  }
+  std::vector<double> x0((size_t)N);
+  for (int i = 0; i < NA; ++i) x0[i] = v->ra[i];  // bead [1][1], x: row 0 of the host layout
+  for (int b = 0; b < NB; ++b) x0[NA + b] = v->rb[b];
+  HIPCHK(s, hipMemcpy(s->dd_gid, gid, sizeof(int32_t) * N, hipMemcpyHostToDevice));
+  HIPCHK(s, hipMemcpy(s->dd_own, own, (size_t)N, hipMemcpyHostToDevice));
+  HIPCHK(s, hipMemcpy(s->dd_x0, x0.data(), sizeof(double) * N, hipMemcpyHostToDevice));
+  s->K.dd = 1;
+  s->d.gid = s->dd_gid;
+  s->d.dd_own = s->dd_own;
+  s->d.dd_x0 = s->dd_x0;
+  int rc = set_state_impl(s, v);
+  if (rc != KMC_OK) return rc;
+  // the counters' offsets and the running largest complex of this slab's
+  // share (the driver gives the global ones to one slab, zero to the others)
+  Ctl c;
+  HIPCHK(s, hipMemcpy(&c, s->d.ctl, sizeof c, hipMemcpyDeviceToHost));
+  c.off_bond = ctl5[0];
+  c.off_rl = ctl5[1];
+  c.off_cis = ctl5[2];
+  c.off_mono = ctl5[3];
+  c.maxc = ctl5[4];
+  c.dd_xcol = c.dd_xbond = 0;
+  HIPCHK(s, hipMemcpy(s->d.ctl, &c, sizeof c, hipMemcpyHostToDevice));
+  return KMC_OK;
+}
+
+int kmc_dd_export(kmc_sim* s, int32_t n, const int32_t* ids, double* beads, int32_t* ints) {
+  if (!s || n < 0 || (n > 0 && (!ids || !beads || !ints))) return KMC_ERR_ARG;
+  if (!s->have_state || !s->K.dd) return fail(s, KMC_ERR_ARG, "dd: no decomposed state");
+  if (n == 0) return KMC_OK;
+  for (int32_t i = 0; i < n; ++i)
+    if (ids[i] < 0 || ids[i] >= s->K.N) return fail(s, KMC_ERR_ARG, "dd: index out of range");
+  int rc = dd_stage(s, n);
+  if (rc != KMC_OK) return rc;
+  HIPCHK(s, hipMemcpyAsync(s->dd_ids, ids, sizeof(int32_t) * n, hipMemcpyHostToDevice, s->stream));
+  k_dd_export<<<(unsigned)(((size_t)n * 48 + 255) / 256), 256, 0, s->stream>>>(s->K, s->d, n, s->dd_ids,
+                                                                            s->dd_beads, s->dd_ints);
+  HIPCHK(s, hipGetLastError());
+  HIPCHK(s, hipMemcpyAsync(beads, s->dd_beads, sizeof(double) * 48 * n, hipMemcpyDeviceToHost, s->stream));
+  HIPCHK(s, hipMemcpyAsync(ints, s->dd_ints, sizeof(int32_t) * 8 * n, hipMemcpyDeviceToHost, s->stream));
+  HIPCHK(s, hipStreamSynchronize(s->stream));
+  return KMC_OK;
+}
+
+int kmc_dd_import(kmc_sim* s, int32_t n, const int32_t* ids, const double* beads, const int32_t* ints,
+                  uint8_t* flags) {
+  if (!s || n < 0 || (n > 0 && (!ids || !beads || !ints || !flags))) return KMC_ERR_ARG;
+  if (!s->have_state || !s->K.dd) return fail(s, KMC_ERR_ARG, "dd: no decomposed state");
+  if (n == 0) return KMC_OK;
+  for (int32_t i = 0; i < n; ++i) {
+    if (ids[i] < 0 || ids[i] >= s->K.N) return fail(s, KMC_ERR_ARG, "dd: index out of range");
+    const bool rec = ids[i] < s->K.NA;
+    for (int f = 0; f < 8; ++f) {
+      const bool link = rec ? (f == 2 || f == 4) : f >= 4;
+      if (link && (ints[(size_t)i * 8 + f] < 0 || ints[(size_t)i * 8 + f] > s->K.N))
+        return fail(s, KMC_ERR_ARG, "dd: link out of range");
+    }
+  }
+  int rc = dd_stage(s, n);
+  if (rc != KMC_OK) return rc;
+  HIPCHK(s, hipMemcpyAsync(s->dd_ids, ids, sizeof(int32_t) * n, hipMemcpyHostToDevice, s->stream));
+  HIPCHK(s, hipMemcpyAsync(s->dd_beads, beads, sizeof(double) * 48 * n, hipMemcpyHostToDevice, s->stream));
+  HIPCHK(s, hipMemcpyAsync(s->dd_ints, ints, sizeof(int32_t) * 8 * n, hipMemcpyHostToDevice, s->stream));
+  HIPCHK(s, hipMemsetAsync(s->dd_flags, 0, ((size_t)n + 3) & ~(size_t)3, s->stream));
+  k_dd_import<<<(unsigned)(((size_t)n * 48 + 255) / 256), 256, 0, s->stream>>>(s->K, s->d, n, s->dd_ids,
+                                                                            s->dd_beads, s->dd_ints, s->dd_flags);
+  HIPCHK(s, hipGetLastError());
+  HIPCHK(s, hipMemcpyAsync(flags, s->dd_flags, (size_t)n, hipMemcpyDeviceToHost, s->stream));
+  HIPCHK(s, hipStreamSynchronize(s->stream));
+  bool links = false;
+  for (int32_t i = 0; i < n; ++i) links |= (flags[i] & 2) != 0;
+  // the chunk snapshot no longer describes this state (a replay from it would
+  // miss the import); kept complexes are rebuilt when a bond of a halo
+  // protein differed
+  s->snap_valid = false;
+  if (links) s->need_full = true;
+  s->clusters_valid = false;
+  return KMC_OK;
+}
+
+int kmc_dd_drift(kmc_sim* s, double* max_dx) {
+  if (!s || !max_dx) return KMC_ERR_ARG;
+  if (!s->have_state || !s->K.dd) return fail(s, KMC_ERR_ARG, "dd: no decomposed state");
+  HIPCHK(s, hipMemsetAsync(s->dd_scratch, 0, sizeof(uint32_t), s->stream));
+  k_dd_drift<<<(s->K.N + 255) / 256, 256, 0, s->stream>>>(s->K, s->d, s->dd_scratch);
+  HIPCHK(s, hipGetLastError());
+  uint32_t bits = 0;
+  HIPCHK(s, hipMemcpyAsync(&bits, s->dd_scratch, sizeof bits, hipMemcpyDeviceToHost, s->stream));
+  HIPCHK(s, hipStreamSynchronize(s->stream));
+  float f;
+  std::memcpy(&f, &bits, sizeof f);
+  *max_dx = f;
+  return KMC_OK;
+}
+
+int kmc_dd_counters(kmc_sim* s, int64_t* out) {
+  if (!s || !out) return KMC_ERR_ARG;
+  HIPCHK(s, hipStreamSynchronize(s->stream));
+  Ctl c;
+  HIPCHK(s, hipMemcpy(&c, s->d.ctl, sizeof c, hipMemcpyDeviceToHost));
+  out[0] = c.dd_xcol;
+  out[1] = c.dd_xbond;
+  return KMC_OK;
+}
 
 }  // extern "C"

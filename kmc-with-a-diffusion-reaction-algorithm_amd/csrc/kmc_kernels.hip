@@ -106,6 +106,12 @@ struct Dev {
   uint32_t* vtag;       // [N]
   Ctl* ctl;
   struct kmc_obs_dev* obs;
+  // decomposed trajectories (KParams::dd, kmc_dd_set_state), by local reference index: the trajectory's
+  // global reference index (the random-stream key), 1 if this slab owns the protein, x of bead [1][1] when
+  // the slab's window was set (kmc_dd_drift)
+  const int32_t* gid;
+  const uint8_t* dd_own;
+  const double* dd_x0;
 };
 
 // one record (32 B): float reference point, ids, cis site
@@ -151,6 +157,17 @@ __device__ __forceinline__ uint32_t state_of(const Dev& d, int key, uint32_t ste
 __device__ __forceinline__ void set_state(const Dev& d, int key, uint32_t step, uint32_t s) {
   st_state(&d.ustate[key], ((step & 0x3fffffffu) << 2) | s);
 }
+
+// random-stream key of local reference index r: the global reference index
+// when this handle holds one slab's window of a decomposed trajectory (the
+// local numbering is monotone in the global one, so every order comparison
+// of local indices is the global one; only the keyed draws need the map)
+__device__ __forceinline__ uint32_t rkey(const KParams& P, const Dev& d, int r) {
+  return P.dd ? (uint32_t)d.gid[r] : (uint32_t)r;
+}
+// protein of local reference index r is owned by this slab (always, outside
+// a decomposed trajectory)
+__device__ __forceinline__ bool dd_owned(const KParams& P, const Dev& d, int r) { return !P.dd || d.dd_own[r]; }
 
 __device__ __forceinline__ int cell_x(const KParams& P, double x) {
   int c = (int)__builtin_floor((x - P.gx0) / P.cs);
@@ -674,9 +691,9 @@ __device__ void propose_free_a(const KParams& P, const Dev& d, int i, uint32_t s
     }
   const uint2 h = d.home[i];
   double u0, u1, u2, u3;
-  const uint32_t ri = (uint32_t)d.id_of[i];
-  kmcr::uniform2(P.key, kmcr::DOM_DIFF, ri, 0, step, 0, &u0, &u1);
-  kmcr::uniform2(P.key, kmcr::DOM_DIFF, ri, 0, step, 1, &u2, &u3);
+  const uint32_t ri = (uint32_t)d.id_of[i], rk = rkey(P, d, (int)ri);
+  kmcr::uniform2(P.key, kmcr::DOM_DIFF, rk, 0, step, 0, &u0, &u1);
+  kmcr::uniform2(P.key, kmcr::DOM_DIFF, rk, 0, step, 1, &u2, &u3);
   double amp = P.amp_a * u0;
   double phai = u1 * 2 * P.pai;
   double dx = amp * kmcm::cos(phai), dy = amp * kmcm::sin(phai);
@@ -812,9 +829,9 @@ __device__ __forceinline__ bool bond_misaligned(const KParams& P, const S& N, in
 // registers, as for the free units.
 __device__ __forceinline__ void propose_dimer(const KParams& P, const Dev& d, int i, int q, uint32_t step) {
   double u0, u1, u2, u3;
-  const uint32_t ri = (uint32_t)d.id_of[i];
-  kmcr::uniform2(P.key, kmcr::DOM_DIFF, ri, 0, step, 0, &u0, &u1);
-  kmcr::uniform2(P.key, kmcr::DOM_DIFF, ri, 0, step, 1, &u2, &u3);
+  const uint32_t rk = rkey(P, d, d.id_of[i]);
+  kmcr::uniform2(P.key, kmcr::DOM_DIFF, rk, 0, step, 0, &u0, &u1);
+  kmcr::uniform2(P.key, kmcr::DOM_DIFF, rk, 0, step, 1, &u2, &u3);
   double amp = P.amp_cis * u0;
   double phai = u1 * 2 * P.pai;
   double dx = amp * kmcm::cos(phai), dy = amp * kmcm::sin(phai);
@@ -963,7 +980,7 @@ __device__ void propose_free_b(const KParams& P, const Dev& d, int lb, int p, ui
     }
   const uint2 h = d.home[p];
   double u[6];
-  const uint32_t rp = (uint32_t)d.id_of[p];
+  const uint32_t rp = rkey(P, d, d.id_of[p]);
   kmcr::uniform2(P.key, kmcr::DOM_DIFF, rp, 0, step, 0, &u[0], &u[1]);
   kmcr::uniform2(P.key, kmcr::DOM_DIFF, rp, 0, step, 1, &u[2], &u[3]);
   kmcr::uniform2(P.key, kmcr::DOM_DIFF, rp, 0, step, 2, &u[4], &u[5]);
@@ -1936,8 +1953,9 @@ __device__ __forceinline__ void cx_params(const KParams& P, const Dev& d, uint32
       continue;
     }
     double u0, u1, u2, u3;
-    kmcr::uniform2(P.key, kmcr::DOM_DIFF, (uint32_t)desc.w, 0, step, 0, &u0, &u1);
-    kmcr::uniform2(P.key, kmcr::DOM_DIFF, (uint32_t)desc.w, 0, step, 1, &u2, &u3);
+    const uint32_t rk = rkey(P, d, desc.w);
+    kmcr::uniform2(P.key, kmcr::DOM_DIFF, rk, 0, step, 0, &u0, &u1);
+    kmcr::uniform2(P.key, kmcr::DOM_DIFF, rk, 0, step, 1, &u2, &u3);
     double amp = (nB == 1 ? P.amp_bond : 0.0) * u0;
     double phai = u1 * 2 * P.pai;
     double dx = amp * kmcm::cos(phai), dy = amp * kmcm::sin(phai);
@@ -2118,14 +2136,14 @@ __global__ void __launch_bounds__(256, HEAVY_WAVES) k_complex_heavy(KParams P, D
     for (int q = lane; q < csize; q += 64) grow[q] = brow[q];
     if (lane == 0) d.shuf_tag[lb] = step;
     wave_sync();
-    cx_rigid<false>(P, d, L, grow, csize, nB, (uint32_t)d.id_of[NA + lb], step, lane,
+    cx_rigid<false>(P, d, L, grow, csize, nB, rkey(P, d, d.id_of[NA + lb]), step, lane,
                     cx_bead0<false>(P, d, L, grow, csize, lane));
     wave_sync();
     if (lane == 0) {
       int pA = -1;  // last receptor in member order (main.cpp:1107, 1147)
       for (int q = csize - 1; q >= 0 && pA < 0; --q)
         if (grow[q] < NA) pA = grow[q];
-      CxT<Beads, GlbLinks> X{P, step, (uint32_t)d.id_of[NA + lb], grow, csize, d.nxt, GlbLinks{&d, NA, NB, step},
+      CxT<Beads, GlbLinks> X{P, step, rkey(P, d, d.id_of[NA + lb]), grow, csize, d.nxt, GlbLinks{&d, NA, NB, step},
                              &d.ctl->err};
       complex_align(X, nB, lb, pA);
     }
@@ -2178,7 +2196,7 @@ __global__ void __launch_bounds__(256, HEAVY_WAVES) k_complex_heavy(KParams P, D
       for (int e = lane; e < CX_SHUF * CXL; e += 64) {
         const int call = e / CXL, pos = e % CXL;
         if (pos >= 1 && pos < csize - 1)
-          L->rnd[call][pos] = kmcr::rand31(P.key, kmcr::DOM_SHUF, (uint32_t)desc.w, call, step, pos);
+          L->rnd[call][pos] = kmcr::rand31(P.key, kmcr::DOM_SHUF, rkey(P, d, desc.w), call, step, pos);
       }
     wave_sync();
     CXS(0);
@@ -2186,7 +2204,7 @@ __global__ void __launch_bounds__(256, HEAVY_WAVES) k_complex_heavy(KParams P, D
       // the last receptor in member order: the highest lane holding one
       const uint64_t rm = __ballot(lane < csize && L->slot[lane] < NA);
       const int pA = rm ? 63 - __clzll((long long)rm) : -1;
-      CxT<LdsBeads, LdsLinks> X{P, step, (uint32_t)desc.w, L->res, csize, LdsBeads{L}, LdsLinks{L, NA}, &d.ctl->err,
+      CxT<LdsBeads, LdsLinks> X{P, step, rkey(P, d, desc.w), L->res, csize, LdsBeads{L}, LdsLinks{L, NA}, &d.ctl->err,
                                 L->rnd};
       if (P.cx_serial) {  // debug (KMC_CX_SERIAL=1): the one-lane alignment
         if (lane == 0) complex_align(X, nB, 0, pA);
@@ -3164,6 +3182,7 @@ __device__ __forceinline__ void col_exact_one(const KParams& P, const Dev& d, in
     if (hit) atomicAdd(&d.ctl->cand_kind[2 * kk + 1], 1u);
   }
   if (!hit) return;
+  if (P.dd && d.dd_own[u] != d.dd_own[kq]) atomicAdd(&d.ctl->dd_xcol, 1u);  // an owned unit against a halo unit
   if (kq >= u) {
     mark_rej(d, u, tag);
     return;
@@ -3392,8 +3411,10 @@ __device__ __forceinline__ void rej_copy(const KParams& P, const Dev& d, int m, 
 #ifndef REJ_LANES  // (A/B, profiles/r04/ab_r4x: 16 -> 32 lanes, k_rej_commit 21.2 -> 18.4 us at C3)
 #define REJ_LANES 32
 #endif
-#ifndef REJ_SIDE  // k_rej_commit on a second stream beside k_rxn_exact .. k_finalize (kmc_engine.hip)
-#define REJ_SIDE 0
+#if defined(REJ_SIDE) && REJ_SIDE
+// (measured round 4 and removed: the revert beside k_rxn_exact .. k_finalize races with the association snaps
+// of k_match, which move receptors in R_new that a revert must restore first — DESIGN.md §8)
+#error "REJ_SIDE is wrong by design"
 #endif
 #ifndef REJ_UNROLL  // rejected units whose lookups a lane group has in flight at once
 #define REJ_UNROLL 1
@@ -3648,8 +3669,8 @@ __global__ void k_rxn_exact(KParams P, Dev d) {
     if (P.dbg_cand) atomicAdd(&d.ctl->rxn_kind[1], 1u);
     const int i = ra.x & RID_PID, q = rb.x & RID_PID;
     // final positions: the proposal (R_new) of an accepted unit, R of a
-    // rejected one — read where they are, so that k_rej_commit's R -> R_new
-    // revert may run at the same time (REJ_SIDE)
+    // rejected one — read where they are (the revert has run, but reading R
+    // for a rejected unit is the same value)
     const Beads& NI = ra.x < 0 ? d.nxt : d.cur;
     const Beads& NQ = rb.x < 0 ? d.nxt : d.cur;
     if (q >= NA) {
@@ -3668,7 +3689,7 @@ __global__ void k_rxn_exact(KParams P, Dev d) {
                              NQ.B(lb, 1, 1, 1) - NQ.B(lb, 1, 2, 1), NQ.B(lb, 1, 1, 2) - NQ.B(lb, 1, 2, 2));
         if (!((kmcm::fabs_(pd) < P.thetapd_cut) && (kmcm::fabs_(ot - 180) < P.thetaot_cut))) continue;
         const uint64_t ri = (uint64_t)d.id_of[i], rq = (uint64_t)d.id_of[q];
-        double u = kmcr::uniform(P.key, kmcr::DOM_RL, (uint32_t)ri, (uint32_t)rq, step, (uint32_t)k);
+        double u = kmcr::uniform(P.key, kmcr::DOM_RL, rkey(P, d, (int)ri), rkey(P, d, (int)rq), step, (uint32_t)k);
         if (!(u < P.p_ass)) continue;
         if (P.dbg_cand) atomicAdd(&d.ctl->rxn_kind[3], 1u);
         uint32_t pos = atomicAdd(&d.ctl->n_rl, 1u);
@@ -3687,8 +3708,9 @@ __global__ void k_rxn_exact(KParams P, Dev d) {
                            NQ.A(q, 3, 1, 1) - NQ.A(q, 3, 3, 1), NQ.A(q, 3, 1, 2) - NQ.A(q, 3, 3, 2));
       if (!(kmcm::fabs_(ot - 180) < P.cis_theta_cut)) continue;
       const uint64_t ri = (uint64_t)d.id_of[i], rq = (uint64_t)d.id_of[q];
-      double um = kmcr::uniform(P.key, kmcr::DOM_MONO, (uint32_t)ri, (uint32_t)rq, step, 0);
-      double uc = kmcr::uniform(P.key, kmcr::DOM_CIS, (uint32_t)ri, (uint32_t)rq, step, 0);
+      const uint32_t gi = rkey(P, d, (int)ri), gq = rkey(P, d, (int)rq);
+      double um = kmcr::uniform(P.key, kmcr::DOM_MONO, gi, gq, step, 0);
+      double uc = kmcr::uniform(P.key, kmcr::DOM_CIS, gi, gq, step, 0);
       uint64_t fl = (um < P.p_mono ? 1u : 0u) | (uc < P.p_cis ? 2u : 0u);
       if (!fl) continue;
       if (P.dbg_cand) atomicAdd(&d.ctl->rxn_kind[3], 1u);
@@ -3859,6 +3881,8 @@ __device__ void rl_match(const KParams& P, const Dev& d) {
   auto apply = [&](uint64_t key) {
     int i = d.slot_of[(int)(key >> 34)], q = d.slot_of[(int)((key >> 2) & 0xffffffffu)], k = (int)(key & 3) + 2;
     int lb = q - NA;
+    if (P.dd && d.dd_own[(int)(key >> 34)] != d.dd_own[(int)((key >> 2) & 0xffffffffu)])
+      atomicAdd(&d.ctl->dd_xbond, 1u);  // a bond between an owned and a halo protein: the slabs re-partition
     A_ST2(d, i) = 1;
     B_ST(d, lb, k) = 1;
     B_NEI(d, lb, k) = i + 1;
@@ -3907,6 +3931,8 @@ __device__ void cis_match(const KParams& P, const Dev& d) {
     uint32_t n = m;
     auto apply = [&](uint64_t key) {
       int i = d.slot_of[(int)(key >> 34)], q = d.slot_of[(int)((key >> 2) & 0xffffffffu)];
+      if (P.dd && d.dd_own[(int)(key >> 34)] != d.dd_own[(int)((key >> 2) & 0xffffffffu)])
+        atomicAdd(&d.ctl->dd_xbond, 1u);
       A_ST3(d, i) = 1;
       A_ST3(d, q) = 1;
       A_NEI3(d, q) = i + 1;
@@ -3937,8 +3963,8 @@ __device__ __forceinline__ bool cis_diss(const KParams& P, const Dev& d, int i, 
   const int NA = P.NA;
   uint32_t dom = mono ? kmcr::DOM_MD : kmcr::DOM_CD;
   double pd = mono ? P.p_mdiss : P.p_cdiss;
-  double ui = kmcr::uniform(P.key, dom, (uint32_t)d.id_of[i], 0, step, 0);
-  double uq = kmcr::uniform(P.key, dom, (uint32_t)d.id_of[q], 0, step, 0);
+  double ui = kmcr::uniform(P.key, dom, rkey(P, d, d.id_of[i]), 0, step, 0);
+  double uq = kmcr::uniform(P.key, dom, rkey(P, d, d.id_of[q]), 0, step, 0);
   if (ui < pd || uq < pd) {
     A_ST3(d, i) = 0;
     A_ST3(d, q) = 0;
@@ -3960,7 +3986,7 @@ __global__ void __launch_bounds__(1024) k_match(KParams P, Dev d) {
 
 // R–L dissociation draw of receptor i (bonded), main.cpp:2063-2092
 __device__ __forceinline__ bool rl_breaks(const KParams& P, const Dev& d, int i, uint32_t step) {
-  return kmcr::uniform(P.key, kmcr::DOM_RLD, (uint32_t)d.id_of[i], 0, step, 0) < P.p_diss;
+  return kmcr::uniform(P.key, kmcr::DOM_RLD, rkey(P, d, d.id_of[i]), 0, step, 0) < P.p_diss;
 }
 
 // ================================================================ 7. observables
@@ -4003,18 +4029,21 @@ __global__ void __launch_bounds__(256) k_diss_observe(KParams P, Dev d) {
       mark_bond_change(P, d, q, step);
       st2_i = 0;
     }
-    v[0] = st2_i;
+    // a decomposed trajectory counts the bonds of the receptors its slab owns,
+    // a cis pair at the owner of its lower reference index (dd_owned)
+    v[0] = dd_owned(P, d, d.id_of[i]) ? st2_i : 0;
     if (A_ST3(d, i) == 1) {
       int q = A_NEI3(d, i) - 1;
       if (i < q) {
         int st2_q = A_ST2(d, q);
         if (st2_q == 1 && rl_breaks(P, d, q, step)) st2_q = 0;
         const bool mono = st2_i == 0 && st2_q == 0;
-        if (!cis_diss(P, d, i, q, mono, step)) v[mono ? 1 : 2] = 1;
+        if (!cis_diss(P, d, i, q, mono, step)) v[mono ? 1 : 2] = dd_owned(P, d, min(d.id_of[i], d.id_of[q])) ? 1 : 0;
       }
     }
   } else if (p < P.N) {
     uint8_t k = d.ukind[p];
+    if (!dd_owned(P, d, d.id_of[p])) k = U_NONE;  // a unit (root ligand) of another slab
     if (k == U_COMPLEX) {
       int s = d.cx_size[p - NA];
       v[3] = s;

@@ -75,6 +75,11 @@ def load_library(path: Optional[str] = None):
     L.kmc_host_write_parameter_log.argtypes = [P(capi.Params), C.c_char_p]
     L.kmc_host_append_gro.argtypes = [P(capi.Params), P(capi.StateView), C.c_char_p]
     L.kmc_host_append_cluster_log.argtypes = [P(capi.Params), C.c_int64, C.c_void_p, C.c_void_p, C.c_char_p]
+    L.kmc_dd_set_state.argtypes = [C.c_void_p, P(capi.StateView), C.c_void_p, C.c_void_p, C.c_void_p]
+    L.kmc_dd_export.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.kmc_dd_import.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.kmc_dd_drift.argtypes = [C.c_void_p, P(C.c_double)]
+    L.kmc_dd_counters.argtypes = [C.c_void_p, C.c_void_p]
     for f in ("kmc_host_math", "kmc_device_math"):
         getattr(L, f).argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]
     _lib = L
@@ -259,6 +264,47 @@ class Simulation:
     @property
     def current_step(self) -> int:
         return int(load_library().kmc_current_step(self._h))
+
+    # ---- one slab's window of a decomposed trajectory (kmc_dd_*, slabs.py)
+    def dd_set_state(self, hs: capi.HostState, gid: np.ndarray, own: np.ndarray, ctl5) -> None:
+        gid = np.ascontiguousarray(gid, dtype=np.int32)
+        own = np.ascontiguousarray(own, dtype=np.uint8)
+        c5 = np.ascontiguousarray(ctl5, dtype=np.int32)
+        n = self.params.n_a + self.params.n_b
+        if gid.size != n or own.size != n or c5.size != 5:
+            raise ValueError("dd_set_state: gid / own sized n_a + n_b, ctl5 five values")
+        v = hs.view()
+        self._check(load_library().kmc_dd_set_state(self._h, C.byref(v), gid.ctypes.data, own.ctypes.data,
+                                                    c5.ctypes.data))
+
+    def dd_export(self, ids: np.ndarray):
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        beads = np.zeros((ids.size, 48), dtype=np.float64)
+        ints = np.zeros((ids.size, 8), dtype=np.int32)
+        self._check(load_library().kmc_dd_export(self._h, ids.size, ids.ctypes.data, beads.ctypes.data,
+                                                 ints.ctypes.data))
+        return beads, ints
+
+    def dd_import(self, ids: np.ndarray, beads: np.ndarray, ints: np.ndarray) -> np.ndarray:
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        beads = np.ascontiguousarray(beads, dtype=np.float64)
+        ints = np.ascontiguousarray(ints, dtype=np.int32)
+        if beads.shape != (ids.size, 48) or ints.shape != (ids.size, 8):
+            raise ValueError("dd_import: beads [n, 48], ints [n, 8]")
+        flags = np.zeros(ids.size, dtype=np.uint8)
+        self._check(load_library().kmc_dd_import(self._h, ids.size, ids.ctypes.data, beads.ctypes.data,
+                                                 ints.ctypes.data, flags.ctypes.data))
+        return flags
+
+    def dd_drift(self) -> float:
+        x = C.c_double()
+        self._check(load_library().kmc_dd_drift(self._h, C.byref(x)))
+        return float(x.value)
+
+    def dd_counters(self):
+        out = np.zeros(2, dtype=np.int64)
+        self._check(load_library().kmc_dd_counters(self._h, out.ctypes.data))
+        return int(out[0]), int(out[1])
 
     def set_timing(self, kernels=(), every: int = 1):
         """Bracket the named kernels with HIP events (empty: off), in every
