@@ -211,6 +211,9 @@ int kmc_host_validate(const kmc_params* p, const kmc_state_view* v);
  *                     this handle's own result, 2 where a status / link did.
  *   kmc_dd_drift      the largest periodic x displacement of an owned
  *                     protein since kmc_dd_set_state.
+ *   kmc_dd_jumpers    the owned proteins displaced more than S since then:
+ *                     *n of them (may exceed cap), the first cap as (local
+ *                     index, x of bead [1][1]).
  *   kmc_dd_counters   out[0] collisions between an owned and a halo unit,
  *                     out[1] bonds formed between an owned and a halo protein,
  *                     both since kmc_dd_set_state. */
@@ -220,6 +223,7 @@ int kmc_dd_export(kmc_sim* s, int32_t n, const int32_t* ids, double* beads, int3
 int kmc_dd_import(kmc_sim* s, int32_t n, const int32_t* ids, const double* beads, const int32_t* ints,
                   uint8_t* flags);
 int kmc_dd_drift(kmc_sim* s, double* max_dx);
+int kmc_dd_jumpers(kmc_sim* s, double S, int32_t cap, int32_t* ids, double* xs, int32_t* n);
 int kmc_dd_counters(kmc_sim* s, int64_t* out);
 
 /* Diagnostics: the portable math of kmc_math.h evaluated on the host and on

@@ -1291,6 +1291,25 @@ __global__ void k_dd_drift(KParams P, Dev d, uint32_t* out) {
   if (__lane_id() == 0) atomicMax(out, __float_as_uint(m));
 }
 
+// the owned proteins whose [1][1] is more than S from its x at the window's
+// set (periodic in x): {local index, x} (slabs.py checks them against the
+// windows)
+__global__ void k_dd_jumpers(KParams P, Dev d, double S, int cap, int32_t* ids, double* xs, uint32_t* cnt) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P.N) return;
+  const int r = d.id_of[p];
+  if (!d.dd_own[r]) return;
+  const double x = d.cur.P(p, 1, 1, 0);
+  double dx = x - d.dd_x0[r];
+  dx = dx - P.box_x * kmcm::round_(dx / P.box_x);
+  if (!(kmcm::fabs_(dx) > S)) return;
+  const uint32_t k = atomicAdd(cnt, 1u);
+  if (k < (uint32_t)cap) {
+    ids[k] = r;
+    xs[k] = x;
+  }
+}
+
 extern "C" {
 
 static int dd_stage(kmc_sim* s, int32_t n) {
@@ -1416,6 +1435,27 @@ int kmc_dd_drift(kmc_sim* s, double* max_dx) {
   float f;
   std::memcpy(&f, &bits, sizeof f);
   *max_dx = f;
+  return KMC_OK;
+}
+
+int kmc_dd_jumpers(kmc_sim* s, double S, int32_t cap, int32_t* ids, double* xs, int32_t* n) {
+  if (!s || cap < 0 || !n || (cap > 0 && (!ids || !xs))) return KMC_ERR_ARG;
+  if (!s->have_state || !s->K.dd) return fail(s, KMC_ERR_ARG, "dd: no decomposed state");
+  int rc = dd_stage(s, cap);
+  if (rc != KMC_OK) return rc;
+  HIPCHK(s, hipMemsetAsync(s->dd_scratch + 1, 0, sizeof(uint32_t), s->stream));
+  k_dd_jumpers<<<(s->K.N + 255) / 256, 256, 0, s->stream>>>(s->K, s->d, S, cap, s->dd_ids, s->dd_beads,
+                                                           s->dd_scratch + 1);
+  HIPCHK(s, hipGetLastError());
+  uint32_t cnt = 0;
+  HIPCHK(s, hipMemcpyAsync(&cnt, s->dd_scratch + 1, sizeof cnt, hipMemcpyDeviceToHost, s->stream));
+  HIPCHK(s, hipStreamSynchronize(s->stream));
+  const int32_t m = (int32_t)std::min<uint32_t>(cnt, (uint32_t)cap);
+  if (m > 0) {
+    HIPCHK(s, hipMemcpy(ids, s->dd_ids, sizeof(int32_t) * m, hipMemcpyDeviceToHost));
+    HIPCHK(s, hipMemcpy(xs, s->dd_beads, sizeof(double) * m, hipMemcpyDeviceToHost));
+  }
+  *n = (int32_t)cnt;  // may exceed cap: the caller asks again with room for all
   return KMC_OK;
 }
 

@@ -80,6 +80,7 @@ def load_library(path: Optional[str] = None):
     L.kmc_dd_import.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     L.kmc_dd_drift.argtypes = [C.c_void_p, P(C.c_double)]
     L.kmc_dd_counters.argtypes = [C.c_void_p, C.c_void_p]
+    L.kmc_dd_jumpers.argtypes = [C.c_void_p, C.c_double, C.c_int32, C.c_void_p, C.c_void_p, P(C.c_int32)]
     for f in ("kmc_host_math", "kmc_device_math"):
         getattr(L, f).argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]
     _lib = L
@@ -305,6 +306,18 @@ class Simulation:
         out = np.zeros(2, dtype=np.int64)
         self._check(load_library().kmc_dd_counters(self._h, out.ctypes.data))
         return int(out[0]), int(out[1])
+
+    def dd_jumpers(self, S: float):
+        """(local ids, x) of the owned proteins displaced more than S Å."""
+        cap = 256
+        while True:
+            ids = np.zeros(cap, dtype=np.int32)
+            xs = np.zeros(cap, dtype=np.float64)
+            n = C.c_int32()
+            self._check(load_library().kmc_dd_jumpers(self._h, S, cap, ids.ctypes.data, xs.ctypes.data, C.byref(n)))
+            if n.value <= cap:
+                return ids[: n.value], xs[: n.value]
+            cap = n.value
 
     def set_timing(self, kernels=(), every: int = 1):
         """Bracket the named kernels with HIP events (empty: off), in every

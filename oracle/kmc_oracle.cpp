@@ -88,6 +88,10 @@ static void euler(double theta, double phi, double psai, double t[3][3]) {
 struct Rng {
   int mode = 0;  // 0 keyed, 1 stream
   kmcr::Key key{0, 0};
+  // one slab's window of a decomposed trajectory (oracle_dd_set_state): the
+  // global 0-based index of each local protein keys its streams
+  const std::vector<int32_t>* gid = nullptr;
+  uint32_t G(int i0) const { return gid ? (uint32_t)(*gid)[i0] : (uint32_t)i0; }
   uint64_t t = 0;  // stream clock
   uint64_t ndraw = 0;
   kmcg::GlibcRand grand{1};
@@ -103,17 +107,19 @@ struct Rng {
     ++ndraw;
     if (mode) return stream_draw();
     double u0, u1;
-    kmcr::uniform2(key, kmcr::DOM_DIFF, (uint32_t)(trig - 1), 0, step, (uint32_t)(slot >> 1), &u0, &u1);
+    kmcr::uniform2(key, kmcr::DOM_DIFF, G(trig - 1), 0, step, (uint32_t)(slot >> 1), &u0, &u1);
     return (slot & 1) ? u1 : u0;
   }
   double pair(uint32_t dom, int a, int b, uint32_t step, uint32_t sub) {
     ++ndraw;
     if (mode) return stream_draw();
-    return kmcr::uniform(key, dom, (uint32_t)(a - 1), (uint32_t)(b - 1), step, sub);
+    // (dissociation draws pass b = 1: a constant, not a protein)
+    const bool pair2 = dom == kmcr::DOM_RL || dom == kmcr::DOM_MONO || dom == kmcr::DOM_CIS;
+    return kmcr::uniform(key, dom, G(a - 1), pair2 ? G(b - 1) : (uint32_t)(b - 1), step, sub);
   }
   int shuf(int root, uint32_t call, uint32_t step, uint32_t pos) {
     if (mode) return grand.next();
-    return (int)kmcr::rand31(key, kmcr::DOM_SHUF, (uint32_t)(root - 1), call, step, pos);
+    return (int)kmcr::rand31(key, kmcr::DOM_SHUF, G(root - 1), call, step, pos);
   }
   double init(int p, uint32_t attempt, int slot) {
     ++ndraw;
@@ -152,6 +158,17 @@ struct Oracle {
   enum { EV_FREE_A, EV_DIMER, EV_FREE_B, EV_COMPLEX, EV_LAYDOWN, EV_MULTI, EV_REPEAT, EV_REJECT,
          EV_RL, EV_MONO, EV_CIS, EV_RLD, EV_MD, EV_CD, EV_SNAP_BOND, EV_SNAP_CIS, EV_N };
   int64_t ev[EV_N] = {0};
+  // decomposed trajectory (oracle_dd_*; the engine's kmc_dd_* contract): the
+  // window's global indices, the proteins this slab owns (1-based), the
+  // counters' offsets of this slab's share, x at the window's set, and the
+  // collisions / bonds between an owned and a halo unit since then
+  bool dd = false;
+  std::vector<int32_t> dd_gid;
+  std::vector<uint8_t> dd_own;
+  std::vector<double> dd_x0;
+  int dd_off[4] = {0, 0, 0, 0};
+  int64_t dd_xcol = 0, dd_xbond = 0;
+  bool owned(int p) const { return !dd || dd_own[p]; }
 
   inline size_t I(int p, int j, int k) const { return ((size_t)p * 5 + j) * 5 + k; }
   inline int& ST(int p, int j) { return st[(size_t)p * 5 + j]; }
@@ -280,10 +297,17 @@ struct Oracle {
   // Does member m (at its R_new) collide with anything?  `unit` lists the
   // members of the unit being moved (their R_new are proposals and they are
   // not yet at their new cells).
+  // a collision found (decomposed trajectory: counted when it pairs an owned
+  // with a halo protein — diagnostics)
+  bool hit(int m, int q) {
+    if (!pair_collides(m, q)) return false;
+    if (dd && dd_own[m] != dd_own[q]) ++dd_xcol;
+    return true;
+  }
   bool member_collides(int m, const std::vector<int>& unit) {
     if (nbmode == 0) {
       for (int q = 1; q <= N; ++q)
-        if (pair_collides(m, q)) return true;
+        if (hit(m, q)) return true;
       return false;
     }
     check_extent(m, true);
@@ -291,10 +315,10 @@ struct Oracle {
     for (int q : cand) {
       bool in_unit = std::find(unit.begin(), unit.end(), q) != unit.end();
       if (in_unit) continue;  // handled below at the proposed position
-      if (pair_collides(m, q)) return true;
+      if (hit(m, q)) return true;
     }
     for (int q : unit)
-      if (pair_collides(m, q)) return true;
+      if (hit(m, q)) return true;
     return false;
   }
   void unit_done(const std::vector<int>& unit) {
@@ -689,6 +713,7 @@ struct Oracle {
               (kmcm::fabs_(theta_ot2 - 180) < P.bond_thetaot_cutoff)) {
             double prob = rng.pair(kmcr::DOM_RL, i, j, step, (uint32_t)k);
             if (prob < PAss) {
+              if (dd && dd_own[i] != dd_own[j]) ++dd_xbond;
               STN(i, 2) = 1;
               STN(j, k) = 1;
               NEIN(j, k) = i;
@@ -742,6 +767,7 @@ struct Oracle {
           if (kmcm::fabs_(theta_ot2 - 180) < P.cis_thetaot_cutoff) {
             double prob = rng.pair(pass == 0 ? kmcr::DOM_MONO : kmcr::DOM_CIS, i, j, step, 0);
             if (prob < PA) {
+              if (dd && dd_own[i] != dd_own[j]) ++dd_xbond;
               STN(i, 3) = 1;
               STN(j, 3) = 1;
               bond_num_new++;
@@ -813,7 +839,7 @@ struct Oracle {
     std::vector<int>& res = results[ci];
     int csize = (int)res.size(), nA = 0, nB = 0;
     for (int m : res) (m > NA ? nB : nA)++;
-    if (csize > maxc) maxc = csize;
+    if (owned(ci) && csize > maxc) maxc = csize;  // (a decomposed trajectory: this slab's units)
     int pA = 0, pB = 0;
     if (csize == 1) {  // single ligand, main.cpp:905-969
       int b = res[0];
@@ -860,8 +886,10 @@ struct Oracle {
         }
     }
     if (csize > 1) {  // rigid complex move, main.cpp:974-1131
-      tot_cluster_num++;
-      tot_proteins_in_cluster += csize;
+      if (owned(ci)) {
+        tot_cluster_num++;
+        tot_proteins_in_cluster += csize;
+      }
       ev[EV_COMPLEX]++;
       double PBx = 0, PBy = 0;
       double Dcal = nB == 1 ? P.bond_D : 0.0;
@@ -1213,6 +1241,27 @@ struct Oracle {
     o->bond_num_mono_cis = bond_num_mono_cis;
     o->bond_num_cis = bond_num_cis;
     o->bond_num = bond_num;
+    if (dd) {
+      // this slab's share: the bonds of the receptors it owns (a cis pair at
+      // its lower index), plus the offsets it was given (the reference's
+      // incremental counters = loaded value + change of the derived counts)
+      int rl = 0, mono = 0, cis = 0;
+      for (int i = 1; i <= NA; ++i) {
+        if (!dd_own[i]) {
+          continue;
+        }
+        rl += st[(size_t)i * 5 + 2];
+        const int q = nei[(size_t)i * 7 + 3];
+        if (st[(size_t)i * 5 + 3] == 1 && q > i) {
+          if (st[(size_t)i * 5 + 2] == 0 && st[(size_t)q * 5 + 2] == 0) ++mono;
+          else ++cis;
+        }
+      }
+      o->bond_num_rl = rl + dd_off[1];
+      o->bond_num_mono_cis = mono + dd_off[3];
+      o->bond_num_cis = cis + dd_off[2];
+      o->bond_num = (rl + mono + cis) + dd_off[0];
+    }
     o->cluster_size = cluster_size;
     o->protein_num_in_max_complex = maxc;
     o->tot_proteins_in_cluster = tot_proteins_in_cluster;
@@ -1281,6 +1330,119 @@ int oracle_step(oracle_t* h, int64_t n, kmc_obs* obs, uint64_t* hashes) {
     g_err = e.what();
     return e.code;
   }
+}
+
+// one slab's window of a decomposed trajectory (the kmc_dd_* contract of
+// include/kmc.h, on the oracle's arrays)
+int oracle_dd_set_state(oracle_t* h, const kmc_state_view* v, const int32_t* gid, const uint8_t* own,
+                        const int32_t* ctl5) {
+  Oracle& o = *h->o;
+  for (int i = 1; i < o.N; ++i)
+    if (gid[i] <= gid[i - 1]) {
+      g_err = "dd: global indices not increasing";
+      return KMC_ERR_ARG;
+    }
+  o.from_view(v);
+  o.dd = true;
+  o.dd_gid.assign(gid, gid + o.N);
+  o.rng.gid = &o.dd_gid;
+  o.dd_own.assign(o.N + 1, 0);
+  o.dd_x0.assign(o.N + 1, 0.0);
+  for (int p = 1; p <= o.N; ++p) {
+    o.dd_own[p] = own[p - 1];
+    o.dd_x0[p] = o.Rx[o.I(p, 1, 1)];
+  }
+  for (int k = 0; k < 4; ++k) o.dd_off[k] = ctl5[k];
+  o.maxc = ctl5[4];
+  o.dd_xcol = o.dd_xbond = 0;
+  return 0;
+}
+int oracle_dd_export(oracle_t* h, int32_t n, const int32_t* ids, double* beads, int32_t* ints) {
+  Oracle& o = *h->o;
+  for (int32_t t = 0; t < n; ++t) {
+    const int p = ids[t] + 1;
+    double* b = beads + (size_t)t * 48;
+    int32_t* f = ints + (size_t)t * 8;
+    for (int e = 0; e < 48; ++e) b[e] = 0.0;
+    for (int e = 0; e < 8; ++e) f[e] = 0;
+    const int nk = p <= o.NA ? 4 : 2;
+    for (int j = 1; j <= 4; ++j)
+      for (int k = 1; k <= nk; ++k) {
+        const size_t e = (size_t)((j - 1) * nk + (k - 1)) * 3;
+        b[e] = o.Rx[o.I(p, j, k)];
+        b[e + 1] = o.Ry[o.I(p, j, k)];
+        b[e + 2] = o.Rz[o.I(p, j, k)];
+      }
+    if (p <= o.NA) {
+      f[0] = o.ST(p, 2), f[1] = o.ST(p, 3), f[2] = o.NEI(p, 2), f[3] = o.NEI(p, 4), f[4] = o.NEI(p, 3);
+    } else {
+      for (int j = 1; j <= 4; ++j) f[j - 1] = o.ST(p, j), f[4 + j - 1] = o.NEI(p, j);
+    }
+  }
+  return 0;
+}
+int oracle_dd_import(oracle_t* h, int32_t n, const int32_t* ids, const double* beads, const int32_t* ints,
+                     uint8_t* flags) {
+  Oracle& o = *h->o;
+  for (int32_t t = 0; t < n; ++t) {
+    const int p = ids[t] + 1;
+    const double* b = beads + (size_t)t * 48;
+    const int32_t* f = ints + (size_t)t * 8;
+    uint8_t fl = 0;
+    const int nk = p <= o.NA ? 4 : 2;
+    auto put = [&](double& dst, double v) {
+      if (std::memcmp(&dst, &v, sizeof v) != 0) fl |= 1;
+      dst = v;
+    };
+    auto puti = [&](int& dst, int v) {
+      if (dst != v) fl |= 2;
+      dst = v;
+    };
+    for (int j = 1; j <= 4; ++j)
+      for (int k = 1; k <= nk; ++k) {
+        const size_t e = (size_t)((j - 1) * nk + (k - 1)) * 3;
+        put(o.Rx[o.I(p, j, k)], b[e]);
+        put(o.Ry[o.I(p, j, k)], b[e + 1]);
+        put(o.Rz[o.I(p, j, k)], b[e + 2]);
+      }
+    if (p <= o.NA) {
+      puti(o.ST(p, 2), f[0]), puti(o.ST(p, 3), f[1]), puti(o.NEI(p, 2), f[2]), puti(o.NEI(p, 4), f[3]);
+      puti(o.NEI(p, 3), f[4]);
+    } else {
+      for (int j = 1; j <= 4; ++j) puti(o.ST(p, j), f[j - 1]), puti(o.NEI(p, j), f[4 + j - 1]);
+    }
+    flags[t] = fl;
+  }
+  return 0;
+}
+double oracle_dd_drift(oracle_t* h) {
+  Oracle& o = *h->o;
+  double m = 0.0;
+  for (int p = 1; p <= o.N; ++p) {
+    if (!o.dd_own[p]) continue;
+    double dx = o.Rx[o.I(p, 1, 1)] - o.dd_x0[p];
+    dx = dx - o.P.box_x * kmcm::round_(dx / o.P.box_x);
+    m = std::max(m, (double)(float)kmcm::fabs_(dx));
+  }
+  return m;
+}
+int32_t oracle_dd_jumpers(oracle_t* h, double S, int32_t cap, int32_t* ids, double* xs) {
+  Oracle& o = *h->o;
+  int32_t n = 0;
+  for (int p = 1; p <= o.N; ++p) {
+    if (!o.dd_own[p]) continue;
+    const double x = o.Rx[o.I(p, 1, 1)];
+    double dx = x - o.dd_x0[p];
+    dx = dx - o.P.box_x * kmcm::round_(dx / o.P.box_x);
+    if (!(kmcm::fabs_(dx) > S)) continue;
+    if (n < cap) ids[n] = p - 1, xs[n] = x;
+    ++n;
+  }
+  return n;
+}
+void oracle_dd_counters(oracle_t* h, int64_t* out) {
+  out[0] = h->o->dd_xcol;
+  out[1] = h->o->dd_xbond;
 }
 
 uint64_t oracle_hash(oracle_t* h) { return h->o->hash(); }

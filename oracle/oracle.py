@@ -73,6 +73,15 @@ def lib():
         L.oracle_stream_clock.argtypes = [C.c_void_p]
         L.oracle_rand_calls.restype = C.c_uint64
         L.oracle_rand_calls.argtypes = [C.c_void_p]
+        L.oracle_dd_set_state.argtypes = [C.c_void_p, C.POINTER(capi.StateView), C.c_void_p, C.c_void_p,
+                                          C.c_void_p]
+        L.oracle_dd_export.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.oracle_dd_import.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.oracle_dd_drift.restype = C.c_double
+        L.oracle_dd_drift.argtypes = [C.c_void_p]
+        L.oracle_dd_counters.argtypes = [C.c_void_p, C.c_void_p]
+        L.oracle_dd_jumpers.restype = C.c_int32
+        L.oracle_dd_jumpers.argtypes = [C.c_void_p, C.c_double, C.c_int32, C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
 
@@ -128,6 +137,50 @@ class Oracle:
             )
         )
         return obs, hashes
+
+    # ---- one slab's window of a decomposed trajectory (the kmc_dd_* contract;
+    # the same driver, slabs.py, runs it over oracles or over HIP handles)
+    def dd_set_state(self, hs: "capi.HostState", gid, own, ctl5) -> None:
+        gid = np.ascontiguousarray(gid, dtype=np.int32)
+        own = np.ascontiguousarray(own, dtype=np.uint8)
+        c5 = np.ascontiguousarray(ctl5, dtype=np.int32)
+        v = hs.view()
+        self._check(lib().oracle_dd_set_state(self.h, C.byref(v), gid.ctypes.data, own.ctypes.data,
+                                              c5.ctypes.data))
+
+    def dd_export(self, ids):
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        beads = np.zeros((ids.size, 48), dtype=np.float64)
+        ints = np.zeros((ids.size, 8), dtype=np.int32)
+        self._check(lib().oracle_dd_export(self.h, ids.size, ids.ctypes.data, beads.ctypes.data, ints.ctypes.data))
+        return beads, ints
+
+    def dd_import(self, ids, beads, ints):
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        beads = np.ascontiguousarray(beads, dtype=np.float64)
+        ints = np.ascontiguousarray(ints, dtype=np.int32)
+        flags = np.zeros(ids.size, dtype=np.uint8)
+        self._check(lib().oracle_dd_import(self.h, ids.size, ids.ctypes.data, beads.ctypes.data, ints.ctypes.data,
+                                           flags.ctypes.data))
+        return flags
+
+    def dd_drift(self) -> float:
+        return float(lib().oracle_dd_drift(self.h))
+
+    def dd_counters(self):
+        out = np.zeros(2, dtype=np.int64)
+        lib().oracle_dd_counters(self.h, out.ctypes.data)
+        return int(out[0]), int(out[1])
+
+    def dd_jumpers(self, S: float):
+        cap = 256
+        while True:
+            ids = np.zeros(cap, dtype=np.int32)
+            xs = np.zeros(cap, dtype=np.float64)
+            n = int(lib().oracle_dd_jumpers(self.h, S, cap, ids.ctypes.data, xs.ctypes.data))
+            if n <= cap:
+                return ids[:n], xs[:n]
+            cap = n
 
     def set_stream(self, clock: int, rand_calls: int):
         """Resume stream mode at rand2() clock `clock` after `rand_calls` rand()s."""
