@@ -65,6 +65,8 @@ struct kmc_sim {
   // undone chunk); KMC_FULL_BFS=1: every step
   bool need_full = true, always_full = false;
   bool debug_counts = false;  // KMC_DEBUG_COUNTS=1: print the last step's work counts per kmc_step chunk
+  bool debug_sync = false;    // KMC_DEBUG_SYNC=1: synchronise after every kernel, name the one that failed
+  int64_t launch_base = 0;    // (debug_sync) the step the current launch_step simulates
   // the unit tables (ukind, complex rows) describe the current step: false
   // after a new state and after a chunk undone without a kept step
   bool clusters_valid = false;
@@ -130,13 +132,20 @@ int fail(kmc_sim* s, int code, const std::string& m) {
       return fail(s, KMC_ERR_HIP, std::string(#x ": ") + hipGetErrorString(e_));          \
   } while (0)
 
+// Zeroed device buffer.  The zeroing runs on the handle's stream and is
+// waited for: a buffer allocated between steps (list growth, the chunk
+// snapshot, the decomposition's staging) is written right away by work on
+// that non-blocking stream, or by a synchronous copy on the null stream —
+// neither is ordered after a null-stream hipMemset, which another thread's
+// null-stream work can hold back (measured: G handles in G threads).
 template <typename T>
 int dalloc(kmc_sim* s, T** p, size_t n) {
   void* v = nullptr;
   size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
   hipError_t e = hipMalloc(&v, bytes);
   if (e != hipSuccess) return fail(s, KMC_ERR_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
-  e = hipMemset(v, 0, bytes);
+  e = hipMemsetAsync(v, 0, bytes, s->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
   if (e != hipSuccess) return fail(s, KMC_ERR_HIP, std::string("hipMemset: ") + hipGetErrorString(e));
   s->allocs.push_back(v);
   *p = (T*)v;
@@ -381,6 +390,8 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   s->poison = po && *po == '1';
   const char* dc = getenv("KMC_DEBUG_COUNTS");
   s->debug_counts = dc && *dc == '1';
+  const char* dsy = getenv("KMC_DEBUG_SYNC");
+  s->debug_sync = dsy && *dsy == '1';
   // debug: lower the LDS tile capacity so that tiles take the global path
   const char* tc = getenv("KMC_DEBUG_TCAP");
   K.tcap = TCAP;
@@ -457,8 +468,7 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
     // per-tile outlier buckets of the pair scan (counters zero between steps)
     s->ntiles = ((K.ncx + K.tile - 1) / K.tile) * ((K.ncy + K.tile - 1) / K.tile);
     if (dalloc(s, &s->d.tout, (size_t)s->ntiles * TOUT_CAP) != KMC_OK ||
-        dalloc(s, &s->d.tout_n, (size_t)s->ntiles) != KMC_OK ||
-        hipMemset(s->d.tout_n, 0, sizeof(uint32_t) * (size_t)s->ntiles) != hipSuccess) {
+        dalloc(s, &s->d.tout_n, (size_t)s->ntiles) != KMC_OK) {
       kmc_destroy(s);
       return KMC_ERR_HIP;
     }
@@ -783,11 +793,54 @@ struct Bracket {
     }
   }
 };
-#define TIMED(k, ...)            \
-  do {                           \
-    Bracket b_(s, k, s->stream); \
-    __VA_ARGS__;                 \
+#define TIMED(k, ...)                                                                                   \
+  do {                                                                                                  \
+    {                                                                                                   \
+      Bracket b_(s, k, s->stream);                                                                      \
+      __VA_ARGS__;                                                                                      \
+    }                                                                                                   \
+    if (s->debug_sync) {                                                                                \
+      const hipError_t e_ = hipStreamSynchronize(s->stream);                                            \
+      if (e_ != hipSuccess)                                                                             \
+        return fail(s, KMC_ERR_HIP, std::string("KMC_DEBUG_SYNC: ") + KNAMES[k] + " failed in step " +     \
+                                        std::to_string(s->launch_base) + ": " + hipGetErrorString(e_)); \
+    }                                                                                                   \
   } while (0)
+
+// debug (KMC_DEBUG_SYNC=1), after the exact tests: the collision lists'
+// shard counts within capacity, every candidate a record index, every
+// conflict entry / pending unit a unit key of this handle
+static int debug_check_lists(kmc_sim* s) {
+  Dev& d = s->d;
+  const int N = s->K.N;
+  HIPCHK(s, hipStreamSynchronize(s->stream));
+  std::vector<uint32_t> cnt(5 * NSHARD);
+  HIPCHK(s, hipMemcpy(cnt.data(), d.shard_cnt, sizeof(uint32_t) * cnt.size(), hipMemcpyDeviceToHost));
+  const SList* L[5] = {&d.cand, &d.conf, &d.plist, &d.rej, &d.pairs};
+  const char* names[5] = {"cand", "conf", "plist", "rej", "pairs"};
+  char m[300];
+  for (int l = 0; l < 5; ++l) {
+    std::vector<int2> v((size_t)L[l]->cap * NSHARD);
+    HIPCHK(s, hipMemcpy(v.data(), L[l]->data, sizeof(int2) * v.size(), hipMemcpyDeviceToHost));
+    for (int k = 0; k < NSHARD; ++k) {
+      const uint32_t c = std::min(cnt[l * NSHARD + k], L[l]->cap);
+      for (uint32_t t = 0; t < c; ++t) {
+        const int2 e = v[(size_t)k * L[l]->cap + t];
+        const int x = e.x, y = l == 1 ? (e.y & 0x7fffffff) : e.y;
+        bool ok = true;
+        if (l == 0 || l == 4) ok = x >= 0 && x < 2 * N && y >= 0 && y < 2 * N;  // record indices
+        if (l == 1) ok = x >= 0 && x < N && y >= 0 && y < N;                    // unit keys
+        if (l == 2 || l == 3) ok = x >= 0 && x < N;
+        if (!ok) {
+          snprintf(m, sizeof m, "KMC_DEBUG_SYNC: list %s shard %d entry %u = (%d, %d) out of range (N %d) in step %lld",
+                   names[l], k, t, e.x, e.y, N, (long long)s->launch_base);
+          return fail(s, KMC_ERR_HIP, m);
+        }
+      }
+    }
+  }
+  return KMC_OK;
+}
 
 // s->tnow (this step bracketed) is set by the caller
 static int launch_step(kmc_sim* s, bool re_sort) {
@@ -846,12 +899,22 @@ static int launch_step(kmc_sim* s, bool re_sort) {
   TIMED(KI_COL_EXACT, {
 #if DENSE_KERNEL
     k_col_dense<<<64, T, 0, st>>>(K, d);
+    if (s->debug_sync && hipStreamSynchronize(st) != hipSuccess)
+      return fail(s, KMC_ERR_HIP, "KMC_DEBUG_SYNC: k_col_dense failed in step " + std::to_string(s->launch_base));
 #endif
     k_col_exact<<<std::max(gX, 64), T, 0, st>>>(K, d);
   });
+  if (s->debug_sync) {
+    const int rc = debug_check_lists(s);
+    if (rc != KMC_OK) return rc;
+  }
   TIMED(KI_COL_ROUNDS, {
     k_col_round<<<gX, T, 0, st>>>(K, d, 0);
+    if (s->debug_sync && hipStreamSynchronize(st) != hipSuccess)
+      return fail(s, KMC_ERR_HIP, "KMC_DEBUG_SYNC: k_col_round failed in step " + std::to_string(s->launch_base));
     k_col_units<<<gX, T, 0, st>>>(K, d, 0);
+    if (s->debug_sync && hipStreamSynchronize(st) != hipSuccess)
+      return fail(s, KMC_ERR_HIP, "KMC_DEBUG_SYNC: k_col_units failed in step " + std::to_string(s->launch_base));
     k_col_tail<<<1, 1024, 0, st>>>(K, d, 1);
   });
   // (the revert cannot run beside the reactions: an association snaps the
@@ -916,8 +979,7 @@ static int launch_step_graph(kmc_sim* s) {
 // device obs records land in obs_buf.  Returns after the stream has drained,
 // with the control block in ctl_host.
 static int run_chunk(kmc_sim* s, int64_t n, int64_t base) {
-  uint32_t zero = 0;
-  HIPCHK(s, hipMemcpyAsync(&s->d.ctl->obs_idx, &zero, sizeof zero, hipMemcpyHostToDevice, s->stream));
+  HIPCHK(s, hipMemsetAsync(&s->d.ctl->obs_idx, 0, sizeof(uint32_t), s->stream));
   for (int64_t k = 0; k < n; ++k) {
     const bool rs = s->resort_every > 0 && ++s->since_resort >= s->resort_every;
     if (rs) s->since_resort = 0;
@@ -928,7 +990,8 @@ static int run_chunk(kmc_sim* s, int64_t n, int64_t base) {
     // graph replay for the plain steps: no re-sort, no full complex rebuild, no
     // event brackets, no debug poison
     const bool plain = !rs && !s->tnow && !s->poison && !s->need_full && !s->always_full &&
-                       s->K.dbg_stage == 0;
+                       s->K.dbg_stage == 0 && !s->debug_sync;
+    s->launch_base = base + k + 1;
     int rc = (s->use_graphs && plain) ? launch_step_graph(s) : launch_step(s, rs);
     if (rc != KMC_OK) return rc;
   }

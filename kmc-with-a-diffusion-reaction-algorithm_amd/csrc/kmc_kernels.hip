@@ -980,10 +980,10 @@ __device__ void propose_free_b(const KParams& P, const Dev& d, int lb, int p, ui
     }
   const uint2 h = d.home[p];
   double u[6];
-  const uint32_t rp = rkey(P, d, d.id_of[p]);
-  kmcr::uniform2(P.key, kmcr::DOM_DIFF, rp, 0, step, 0, &u[0], &u[1]);
-  kmcr::uniform2(P.key, kmcr::DOM_DIFF, rp, 0, step, 1, &u[2], &u[3]);
-  kmcr::uniform2(P.key, kmcr::DOM_DIFF, rp, 0, step, 2, &u[4], &u[5]);
+  const uint32_t rp = (uint32_t)d.id_of[p], rk = rkey(P, d, (int)rp);  // unit key, random-stream key
+  kmcr::uniform2(P.key, kmcr::DOM_DIFF, rk, 0, step, 0, &u[0], &u[1]);
+  kmcr::uniform2(P.key, kmcr::DOM_DIFF, rk, 0, step, 1, &u[2], &u[3]);
+  kmcr::uniform2(P.key, kmcr::DOM_DIFF, rk, 0, step, 2, &u[4], &u[5]);
   double amp = P.amp_b * u[0];
   double theta = u[1] * P.pai;
   double phai = u[2] * 2 * P.pai;

@@ -49,6 +49,7 @@ torch.distributed).
 """
 from __future__ import annotations
 
+import os
 import threading
 from dataclasses import dataclass, field
 from typing import Callable, List, Optional
@@ -134,6 +135,10 @@ def run_threads(world: int, fn: Callable[[int], object]) -> list:
         t.join()
     if err:
         real = [e for e in err if not isinstance(e, threading.BrokenBarrierError)]
+        if len(real) > 1:
+            real[0].add_note("other ranks: " + "; ".join(repr(e) for e in real[1:])) if hasattr(real[0], "add_note") \
+                else None
+            real[0].args = real[0].args + tuple(f"(also: {e!r})" for e in real[1:])
         raise (real or err)[0]
     return out
 
@@ -308,11 +313,15 @@ class SlabRank:
         self.counters = np.zeros(5, dtype=np.int32)
         self.ckpt: Optional[capi.HostState] = None
         self.history: list = []  # global records since the checkpoint (replay check)
-        self.stats = dict(steps=0, rebuilds=0, rebuild_bond=0, rebuild_jumpers=0, rollbacks=0, xcol=0, xbond=0,
+        self.stats = dict(steps=0, rebuilds=0, rebuild_bond=0, rebuild_jumpers=0, rollbacks=0, replayed=0, xcol=0,
+                          xbond=0,
                           exchanged=0, verified=0, jumpers=0, held=0, owned=0, why=[])
         self.last_global: Optional[capi.HostState] = None
         self._xc = (0, 0)
         self._njump = 0  # jumpers after the last step, all slabs
+        # debug (KMC_SLABS_CHECK=1): the window's bond graph and extent bounds
+        # validated (kmc_host_validate) after every import
+        self.check = os.environ.get("KMC_SLABS_CHECK") == "1"
 
     @property
     def band(self) -> float:
@@ -346,6 +355,7 @@ class SlabRank:
             self.eng.close()
         q = capi.Params.from_buffer_copy(self.p)
         q.n_a, q.n_b = w.n_a, w.n_b
+        self.q = q
         self.eng = self.make_engine(q)
         self.eng.dd_set_state(ws, w.gids, w.own, ctl5)
         self._xc = (0, 0)
@@ -408,9 +418,15 @@ class SlabRank:
             tries += 1
             self._recover(widen=tries > 1)
             rec = self._one()
-        self.history.append(rec.copy())
+        self._remember(rec)
         self.stats["steps"] += 1
         return rec
+
+    def _remember(self, rec: np.ndarray) -> None:
+        # the records since the checkpoint (a re-partition inside the step
+        # made its end state the checkpoint: nothing to replay for it)
+        if int(rec["step"][0]) > self.ckpt.step:
+            self.history.append(rec.copy())
 
     def _one(self) -> Optional[np.ndarray]:
         if self._njump > JUMPERS_MAX:
@@ -483,6 +499,13 @@ class SlabRank:
             bad += int((flags[vb] != 0).sum())
             self.stats["exchanged"] += int(loc.size)
         self.stats["verified"] += nver
+        if self.check:
+            from . import engine as _engine
+
+            rc = _engine.host_validate(self.q, self.eng.get_state())
+            if rc != 0:
+                raise SlabError(f"rank {self.rank}: window state invalid ({rc}) after the import of step "
+                                f"{self.step_no + 1}: {_engine.load_library().kmc_host_last_error().decode()}")
         jbad = self._jumper_check()
         # the step's record from every slab's share; checks, triggers
         shares = self.comm.allgather(self.rank, (part.copy(), bad, jbad, dbond, dcol, self._my_jumpers))
@@ -515,6 +538,7 @@ class SlabRank:
         if self.stats["rollbacks"] > 64 or self.halo > 64 * self.p.box_x:
             raise SlabError("decomposed step does not pass its checks even with the whole box as halo")
         hist = self.history
+        self.stats["replayed"] += len(hist)
         if widen:
             self.halo *= 1.5
         self.counters = self.ckpt.counters.copy()
@@ -523,8 +547,10 @@ class SlabRank:
         for want in hist:
             rec = self._step_exchange()
             if rec is None or not np.array_equal(rec, want):
-                raise SlabError("replaying from the checkpoint did not reproduce the steps already returned")
-            self.history.append(rec.copy())
+                raise SlabError(f"rank {self.rank}: replaying from the checkpoint (step {self.ckpt.step}) did not "
+                                f"reproduce step {int(want['step'][0])}: "
+                                f"{'a check failed' if rec is None else f'{rec} != {want}'}; checks: {self.stats['why']}")
+            self._remember(rec)
         if hist:
             self._rebuild_from(self.global_state())
 
