@@ -32,19 +32,24 @@ def main():
         done += k
         print(f"evolved {done}/{evolve}: bond_num {int(ob[-1]['bond_num'])} ({time.time() - t:.0f}s)", flush=True)
     st = sim.get_state()
-    obs = sim.step(window)
-    h = engine.state_hash(p, sim.get_state())
+    obs, hashes = [], []
+    for _ in range(window):  # one step at a time: every step's full-state hash
+        obs.append(sim.step(1)[0])
+        hashes.append(engine.state_hash(p, sim.get_state()))
+    h = hashes[-1]
     sim.close()
     o = O.Oracle(p, nbmode=O.NB_CELLS)
     o.set_state(st)
     print(f"oracle loaded ({time.time() - t:.0f}s)", flush=True)
     ok = True
     for s in range(window):
-        obs_o, _ = o.step(1, want_hashes=False)
+        obs_o, hs_o = o.step(1)
         same = obs[s] == obs_o[0]
-        ok &= bool(same)
-        print(f"step {evolve + s + 1}: {'equal' if same else 'DIFFERENT'} bond.dat record "
-              f"(bond_num {int(obs[s]['bond_num'])}) ({time.time() - t:.0f}s)", flush=True)
+        hsame = hashes[s] == int(hs_o[0])
+        ok &= bool(same) and hsame
+        print(f"step {evolve + s + 1}: {'equal' if same else 'DIFFERENT'} bond.dat record {obs[s]} "
+              f"(every field), state hash gpu {hashes[s]:x} oracle {int(hs_o[0]):x}: "
+              f"{'equal' if hsame else 'DIFFERENT'} ({time.time() - t:.0f}s)", flush=True)
     hs = o.hash()
     print(f"state hash gpu {h:x} oracle {hs:x}: {'equal' if h == hs else 'DIFFERENT'}", flush=True)
     print("window events", o.stats(), flush=True)
