@@ -63,7 +63,6 @@ def kernel_bytes(name: str, n_a: int, n_b: int):
         "k_propose": 768 * n_a + 384 * n_b + n + 8 * n + 64 * n,
         # every record once (float4 + id + site)
         "k_pair_scan": 2 * n * 32,
-        "k_commit": 8 * n,
         "k_classify": 20 * n_a + 12 * n_b + 5 * n,
         "k_observe": 16 * n_a + 5 * n_b,
     }
@@ -95,7 +94,7 @@ def pmc_traffic(kernel: str, workload: str):
 
 def kernel_trace_name(name: str) -> str:
     # engine timing names -> the kernel symbol rocprof reports
-    return {"k_commit": "k_rej_commit"}.get(name, name)
+    return name
 
 
 def parse(argv):

@@ -54,7 +54,7 @@ struct Ctl {
   uint32_t n_overflow;    // ligands whose BFS overflowed the register queue
   uint32_t cx_cursor;     // members[] allocation cursor (rows are kept across steps; k_cx_kill resets)
   uint32_t n_pend;        // units still pending after a round (pass C)
-  uint32_t n_pqu, n_pqe;  // compacted pending units / conflict entries for k_col_tail
+  uint32_t n_pqu, n_pqe;  // compacted pending units / conflict entries for the later rounds
   uint32_t n_cx;          // complexes registered by the BFS this step (cx_list)
   uint32_t n_heavy;       // entries of cx_heavy this step
   uint32_t full_now;      // k_cx_kill: no complex kept this step (every bonded ligand runs the BFS)
@@ -67,9 +67,8 @@ struct Ctl {
   // observable bookkeeping (the per-step counts are reduced by k_finalize)
   int32_t off_bond, off_rl, off_cis, off_mono;  // counters − derived at load
   int32_t maxc;                                 // protein_num_in_Max_Complex
-  uint32_t force_full;    // k_finalize: the next step's k_cx_kill rebuilds every complex (members[] half
-                          // full, or a dirty list overflowed); only k_finalize writes it
-  uint32_t n_forced;      // diagnostics: full complex rebuilds latched by force_full since the state was set
+  uint32_t n_forced;      // diagnostics: full complex rebuilds k_finalize made (members[] half full, or a
+                          // dirty list overflowed) since the state was set
   uint32_t last_outl;     // diagnostics: the previous step's outlier records (n_outl)
   uint32_t cand_kind[6];  // diagnostics (KMC_DEBUG_CAND) since the state was set: collision candidates
                           // of kind pair A-A, A-B, B-B (proposal kind + other kind), tested / colliding

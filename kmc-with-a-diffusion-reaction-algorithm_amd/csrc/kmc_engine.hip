@@ -20,13 +20,13 @@ using namespace kmcd;
 // kernel ids for per-kernel HIP-event timing (kmc_set_timing / kmc_kernel_times)
 enum KId {
   KI_CLASSIFY, KI_BFS, KI_PROPOSE, KI_PROPOSE_FREE, KI_MOVE_MEMBERS, KI_CX_CHECK, KI_CX_HEAVY, KI_CX_KILL,
-  KI_PAIR_SCAN, KI_COL_EXACT, KI_COL_ROUNDS, KI_COMMIT, KI_RXN_EXACT, KI_MATCH, KI_DISS_OBSERVE,
+  KI_PAIR_SCAN, KI_COL_EXACT, KI_COL_ROUNDS, KI_COMMIT, KI_MATCH, KI_DISS_OBSERVE,
   KI_RESORT, KI_N
 };
 static const char* const KNAMES[KI_N] = {
     "k_classify", "k_bfs", "k_propose", "k_propose_free", "k_move_members", "k_cx_check", "k_complex_heavy",
     "k_cx_kill",
-    "k_pair_scan", "k_col_exact", "k_col_rounds", "k_commit", "k_rxn_exact",
+    "k_pair_scan", "k_col_exact", "k_col_rounds", "k_commit_rxn",
     "k_match", "k_diss_observe", "slot_resort"};
 #define TRING 64  // steps of event pairs kept in flight
 
@@ -360,6 +360,7 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   rc |= dalloc(s, &d.bfs_cand, NB);
   rc |= dalloc(s, &d.dlist, 2 * (size_t)N);
   rc |= dalloc(s, &d.pend, N);
+  rc |= dalloc(s, &d.ccnt, N);
   rc |= dalloc(s, &d.overflow, NB);
   rc |= dalloc(s, &d.cx_list, (size_t)d.mcap / 2);  // kept across steps: every registration since the last rebuild
   rc |= dalloc(s, &d.cx_heavy, NB);
@@ -574,6 +575,7 @@ static int clear_step_tags(kmc_sim* s) {
   HIPCHK(s, hipMemsetAsync(d.ustate, 0, sizeof(uint32_t) * N, st));
   HIPCHK(s, hipMemsetAsync(d.moved, 0, sizeof(uint32_t) * N, st));
   HIPCHK(s, hipMemsetAsync(d.pend, 0, sizeof(uint32_t) * N, st));
+  HIPCHK(s, hipMemsetAsync(d.ccnt, 0, sizeof(unsigned long long) * N, st));
   HIPCHK(s, hipMemsetAsync(d.vtag, 0, sizeof(uint32_t) * N, st));
   HIPCHK(s, hipMemsetAsync(d.shard_cnt, 0, sizeof(uint32_t) * 5 * NSHARD, st));
   // BFS candidates and shuffled rows are tagged with the step: an undone
@@ -860,11 +862,12 @@ static int launch_step(kmc_sim* s, bool re_sort) {
     (void)hipMemsetAsync(d.nxt.a, 0xff, sizeof(double) * 48 * bead_slots(K.NA), st);
     (void)hipMemsetAsync(d.nxt.b, 0xff, sizeof(double) * 24 * bead_slots(K.NB), st);
   }
-  if (K.NB > 0) {
-    const int full = (s->need_full || re_sort || s->always_full) ? 1 : 0;
-    s->need_full = false;
-    TIMED(KI_CX_KILL, (k_cx_kill<<<std::min(gN, 1024), T, 0, st>>>(K, d, full)));
-  }
+  // complexes: the previous step's k_finalize dissolved those whose bonds
+  // changed; a full rebuild (after a re-sort, a new state, an undone chunk,
+  // KMC_FULL_BFS) resets them all here
+  if (K.NB > 0 && (s->need_full || re_sort || s->always_full))
+    TIMED(KI_CX_KILL, (k_cx_kill<<<std::min(gN, 1024), T, 0, st>>>(K, d)));
+  s->need_full = false;
   TIMED(KI_CLASSIFY, (k_classify<<<gN, T, 0, st>>>(K, d)));
   // KI_PROPOSE brackets the whole proposal phase: every protein's R read and
   // R_new written once (the bench's roofline unit).  Complexes kept or newly
@@ -909,22 +912,17 @@ static int launch_step(kmc_sim* s, bool re_sort) {
     if (rc != KMC_OK) return rc;
   }
   TIMED(KI_COL_ROUNDS, {
-    k_col_round<<<gX, T, 0, st>>>(K, d, 0);
+    k_col_resolve<<<gX, T, 0, st>>>(K, d);
     if (s->debug_sync && hipStreamSynchronize(st) != hipSuccess)
-      return fail(s, KMC_ERR_HIP, "KMC_DEBUG_SYNC: k_col_round failed in step " + std::to_string(s->launch_base));
-    k_col_units<<<gX, T, 0, st>>>(K, d, 0);
-    if (s->debug_sync && hipStreamSynchronize(st) != hipSuccess)
-      return fail(s, KMC_ERR_HIP, "KMC_DEBUG_SYNC: k_col_units failed in step " + std::to_string(s->launch_base));
+      return fail(s, KMC_ERR_HIP, "KMC_DEBUG_SYNC: k_col_resolve failed in step " + std::to_string(s->launch_base));
     k_col_tail<<<1, 1024, 0, st>>>(K, d, 1);
   });
   // (the revert cannot run beside the reactions: an association snaps the
   // receptor in R_new, and a receptor of a rejected unit must be reverted
   // before that — DESIGN.md §8, the rejected REJ_SIDE variant)
-  TIMED(KI_COMMIT, (k_rej_commit<<<gX, T, 0, st>>>(K, d)));
-  if (K.NA > 0) {
-    TIMED(KI_RXN_EXACT, (k_rxn_exact<<<1024, T, 0, st>>>(K, d)));
-    TIMED(KI_MATCH, (k_match<<<1, 1024, 0, st>>>(K, d)));
-  }
+  // the revert and the exact reaction tests (one launch, k_commit_rxn)
+  TIMED(KI_COMMIT, (k_commit_rxn<<<gX + (K.NA > 0 ? 1024 : 0), T, 0, st>>>(K, d, gX)));
+  if (K.NA > 0) TIMED(KI_MATCH, (k_match<<<1, 1024, 0, st>>>(K, d)));
   TIMED(KI_DISS_OBSERVE, {
     k_diss_observe<<<gN, T, 0, st>>>(K, d);
     k_finalize<<<1, 1024, 0, st>>>(K, d, s->p.time_step, gN);

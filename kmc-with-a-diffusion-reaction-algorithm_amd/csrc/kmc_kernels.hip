@@ -68,6 +68,7 @@ struct Dev {
   uint32_t* bfs_cand;  // [NB] step tag: ligand lb runs the BFS this step
   int32_t* dlist;    // [2][N] proteins whose bonds changed during step s (list s & 1)
   uint32_t* pend;    // [N] round tag: unit still waiting (resolution pass C)
+  unsigned long long* ccnt;  // [N] round 0 of unit u's conflict entries (k_col_resolve; 0 between steps)
   int32_t* overflow; // [NB]
   int4* cx_list;     // [NB] descriptors of the registered complexes (kept across steps; cx_params, k_cx_check)
   int4* cx_heavy;    // [NB] descriptors for k_complex_heavy: larger complexes, and those k_cx_check
@@ -93,8 +94,8 @@ struct Dev {
   SList plist;          // units with conflict entries (u, 0)
   SList rej;            // units rejected this step (u, 0)
   SList pairs;          // reaction candidates (receptor, partner)
-  int32_t* pq_units;    // [N] units still pending after the grid round (k_col_units)
-  int2* pq_ent;         // [conf capacity] conflict entries left pending by round 0 (k_col_round)
+  int32_t* pq_units;    // [N] units still pending after round 0 (k_col_resolve)
+  int2* pq_ent;         // [conf capacity] conflict entries left pending by round 0 (k_col_resolve)
   uint32_t* shard_cnt;  // [5][NSHARD] counters of the lists above
   int32_t* obs_part;    // [blocks][8] per-block observable partials
   uint64_t* rl_keys;    // [cap]
@@ -251,41 +252,42 @@ __global__ void k_classify(KParams P, Dev d) {
 
 // Complexes are kept from step to step: a BFS row depends only on the bond
 // graph, which changes only where a bond formed or broke (k_match,
-// k_diss_observe list those proteins).  Before classification, every
-// complex containing a listed protein is dissolved (its members' croot
-// reset) and its ligands, and the listed ligands, become BFS candidates; the
-// BFS of the candidates (k_bfs) registers the new complexes.  full: no
-// complex is kept (after a re-sort, a new state, an undone chunk — or when the
-// appended rows fill half of members[]): every bonded ligand runs the BFS.
-__global__ void k_cx_kill(KParams P, Dev d, int full) {
-  const int NA = P.NA;
-  const uint32_t step = d.ctl->step;
-  // latched by the previous step's k_finalize: this kernel resets cx_cursor,
-  // so it must not derive the branch from it (blocks would disagree)
-  full |= d.ctl->force_full;
-  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, nt = gridDim.x * blockDim.x;
-  if (full) {
-    for (uint32_t p = tid; p < (uint32_t)P.N; p += nt) d.croot[p] = -1;
-    for (uint32_t b = tid; b < (uint32_t)P.NB; b += nt) d.cx_alive[b] = 0;
-    if (tid == 0) {
-      d.ctl->cx_cursor = 0;
-      d.ctl->n_cx = 0;
-      d.ctl->full_now = 1;
-    }
-    return;
+// k_diss_observe list those proteins).  At the end of each step (k_finalize,
+// cx_dissolve_dirty) every complex containing a listed protein is dissolved
+// (its members' croot reset) and its ligands, and the listed ligands, become
+// BFS candidates of the next step; the BFS of the candidates (k_bfs)
+// registers the new complexes.  A full rebuild — no complex kept — is
+// k_cx_kill: launched by the host before the step after a re-sort, a new
+// state or an undone chunk (and every step with KMC_FULL_BFS=1), or done by
+// k_finalize itself when the appended rows fill half of members[] or a dirty
+// list overflowed: every bonded ligand runs the BFS.
+__device__ __forceinline__ void cx_reset_all(const KParams& P, const Dev& d, uint32_t tid, uint32_t nt) {
+  for (uint32_t p = tid; p < (uint32_t)P.N; p += nt) d.croot[p] = -1;
+  for (uint32_t b = tid; b < (uint32_t)P.NB; b += nt) d.cx_alive[b] = 0;
+  if (tid == 0) {
+    d.ctl->cx_cursor = 0;
+    d.ctl->n_cx = 0;
+    d.ctl->full_now = 1;
   }
-  if (tid == 0) d.ctl->full_now = 0;
-  const uint32_t li = (step + 1) & 1, n = min(d.ctl->n_dirty[li], (uint32_t)P.N);
-  for (uint32_t t = tid; t < n; t += nt) {
+}
+__global__ void k_cx_kill(KParams P, Dev d) {
+  cx_reset_all(P, d, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x);
+}
+// the complexes of the proteins whose bonds changed during `step` (dirty list
+// step & 1), dissolved for step + 1 (k_finalize's workgroup)
+__device__ __forceinline__ void cx_dissolve_dirty(const KParams& P, const Dev& d, uint32_t step) {
+  const int NA = P.NA;
+  const uint32_t li = step & 1, n = min(d.ctl->n_dirty[li], (uint32_t)P.N), next = step + 1;
+  for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) {
     const int p = d.dlist[(size_t)li * P.N + t];
-    if (p >= NA) d.bfs_cand[p - NA] = step;
+    if (p >= NA) d.bfs_cand[p - NA] = next;
     const int r = d.croot[p];
     if (r < 0 || atomicExch(&d.cx_alive[r - NA], 0u) != 1u) continue;
     const int b = r - NA, off = d.cx_off[b], sz = d.cx_size[b];
     for (int i = 0; i < sz; ++i) {
       const int m = d.members[off + i];
       d.croot[m] = -1;
-      if (m >= NA) d.bfs_cand[m - NA] = step;
+      if (m >= NA) d.bfs_cand[m - NA] = next;
     }
   }
 }
@@ -293,7 +295,7 @@ __global__ void k_cx_kill(KParams P, Dev d, int full) {
 // a bond of protein p formed or broke this step (dirty list of step & 1).
 // Without ligands no complex exists and the list is never read.  A list that
 // overflows (a protein can be listed several times) is not an error: the
-// next step rebuilds every complex instead (k_finalize latches force_full).
+// next step rebuilds every complex instead (k_finalize resets them all).
 __device__ __forceinline__ void mark_bond_change(const KParams& P, const Dev& d, int p, uint32_t step) {
   if (P.NB == 0) return;
   const uint32_t li = step & 1;
@@ -2408,11 +2410,15 @@ __device__ __forceinline__ void wg_list_init(WgList& L) {
 __device__ __forceinline__ int my_shard() { return blockIdx.x & (NSHARD - 1); }
 
 // wave-aggregated append of the calling lanes' entries to the workgroup's shard
-__device__ __forceinline__ void sl_push(const SList& s, int2 v, uint32_t* err) {
+__device__ __forceinline__ bool sl_push(const SList& s, int2 v, uint32_t* err) {
   const int k = my_shard();
   const uint32_t pos = wave_slot(&s.cnt[k]);
-  if (pos < s.cap) s.data[(size_t)k * s.cap + pos] = v;
-  else atomicOr(err, ERR_EDGES);
+  if (pos < s.cap) {
+    s.data[(size_t)k * s.cap + pos] = v;
+    return true;
+  }
+  atomicOr(err, ERR_EDGES);
+  return false;
 }
 
 __device__ __forceinline__ uint32_t sl_total(const SList& s) {
@@ -2919,18 +2925,38 @@ __device__ __forceinline__ void item_ranges(const KParams& P, const TileLds& T, 
 #ifndef WALK_BITS  // (A/B builds: 0 = binary search over the lanes' prefix)
 #define WALK_BITS 1
 #endif
+#ifndef WALK_PERM  // (A/B builds: 0 = lane L of wave w takes record base + 4L + w)
+#define WALK_PERM 1
+#endif
+// Item record of lane `lane` of wave `wv` in the 256-record block at `base`
+// (4 waves).  The waves sample the whole block (the staged records are in bin
+// order; each wave should walk about as many pairs as the others), in runs of
+// 16 consecutive records: lane 16g + i takes record 16·((5g + 4wv) mod 16) + i
+// — the four waves' runs {5g + 4wv} cover the 16 runs once — so the owner
+// reads of the walk (T.pos: ds_read_b128, 16-lane groups, banks (a/4) mod 64;
+// T.id, site: ds_read_b64, 32-lane halves) hit distinct banks: a run's 16
+// records fill the 64 banks, and runs r, r + 5 of one half differ in parity
+// (16 records = 128 B apart mod 256 B).  Records base + 4·lane + wv (the
+// round-robin order before) put a group's lanes 64 B apart: 4-way conflicts
+// on every owner read (SQ_LDS_BANK_CONFLICT, profiles/r05/ab_walk).
+__device__ __forceinline__ int walk_item(int base, int lane, int wv, int nw) {
+#if WALK_PERM
+  if (nw == 4) return base + 16 * ((5 * (lane >> 4) + 4 * wv) & 15) + (lane & 15);
+#endif
+  return base + lane * nw + wv;
+}
 template <class Rng, class Chk>
 __device__ __forceinline__ void tile_walk(const TileGeo& G, const TileLds& T, uint32_t* wbits, Rng rng, Chk chk) {
   const int n = T.n, lane = __lane_id();
-  // records go to the waves round-robin (record base + lane·nw + wave): the
-  // staged records are in bin order, so each wave samples the whole block and
-  // the waves of a workgroup walk about the same number of pairs
+  // records go to the waves spread over the block (walk_item): the staged
+  // records are in bin order, so each wave samples the whole block and the
+  // waves of a workgroup walk about the same number of pairs
 #if WALK_STRIDE
   const int nw = blockDim.x >> 6, wv = threadIdx.x >> 6;
 #endif
   for (int base = 0; base < n; base += blockDim.x) {
 #if WALK_STRIDE
-    const int l = base + lane * nw + wv;
+    const int l = walk_item(base, lane, wv, nw);
 #else
     const int l = base + threadIdx.x;
 #endif
@@ -3000,7 +3026,7 @@ __device__ __forceinline__ void tile_walk(const TileGeo& G, const TileLds& T, ui
           if ((int)(v >> 16) <= t) sel = v;
         }
 #if WALK_STRIDE
-        if (q < wtot) chk(base + ((uint32_t)eo >> 24) * nw + wv, (int)(sel & 0xffffu) + t - (int)(sel >> 16));
+        if (q < wtot) chk(walk_item(base, (int)((uint32_t)eo >> 24), wv, nw), (int)(sel & 0xffffu) + t - (int)(sel >> 16));
 #else
         if (q < wtot) chk(l0 + ((uint32_t)eo >> 24), (int)(sel & 0xffffu) + t - (int)(sel >> 16));
 #endif
@@ -3022,7 +3048,7 @@ __device__ __forceinline__ void tile_walk(const TileGeo& G, const TileLds& T, ui
         if ((int)(v >> 16) <= t) sel = v;
       }
 #if WALK_STRIDE
-      if (q < wtot) chk(base + o * nw + wv, (int)(sel & 0xffffu) + t - (int)(sel >> 16));
+      if (q < wtot) chk(walk_item(base, o, wv, nw), (int)(sel & 0xffffu) + t - (int)(sel >> 16));
 #else
       if (q < wtot) chk(l0 + o, (int)(sel & 0xffffu) + t - (int)(sel >> 16));
 #endif
@@ -3189,11 +3215,13 @@ __device__ __forceinline__ void col_exact_one(const KParams& P, const Dev& d, in
   }
   uint32_t old = atomicMax(&d.ustate[u], tag | S_PEND);
   if ((old & ~3u) != tag) {
-    sl_push(d.plist, make_int2(u, 0), &d.ctl->err);  // at most one entry per unit
+    sl_push(d.plist, make_int2(u, 0), &d.ctl->err);  // at most one entry per unit (the step's work counts)
   } else if ((old & 3u) == S_REJ) {
     return;
   }
-  sl_push(d.conf, make_int2(u, kq | (isnew ? (int)0x80000000 : 0)), &d.ctl->err);
+  // each stored entry counted once, taken back by round 0 (k_col_resolve):
+  // the count returns to 0 within the step, an overflowed list included
+  if (sl_push(d.conf, make_int2(u, kq | (isnew ? (int)0x80000000 : 0)), &d.ctl->err)) atomicAdd(&d.ccnt[u], 1ull);
 }
 
 // Records of a dense block's staging sequence (the home records of its home
@@ -3332,40 +3360,60 @@ __device__ __forceinline__ int conf_unit(const Dev& d, int u, uint32_t step, uin
   return 0;
 }
 
-// Round 0 over every conflict entry.  An entry whose kq is still pending is
-// the only kind a later round can change (an entry evaluated against a
-// decided kq has had its effect), so those are compacted for k_col_tail here.
-// The counters n_pend / n_pqu / n_pqe were zeroed by the previous step's
+// Round 0 over every conflict entry, and of every unit as soon as its last
+// entry is evaluated: no grid-wide barrier between the entries and their
+// units.  ccnt[u] packs the round in one word that each entry changes with a
+// single atomic (so no fence orders an entry's effect before its count): the
+// entries not yet evaluated (bits 0-31, counted by k_col_exact), the entries
+// left waiting on a pending kq (32-47), the entries that rejected u (48-63).
+// The entry that takes the count to 0 decides u and clears the word.  A unit
+// decided here may decide a later entry of this round (every deduction is
+// sound in any order, so the outcome is still the sequential one).  An entry
+// whose kq is still pending is the only kind a later round can change, so
+// those, and the units still pending, are compacted for k_col_tail.  The
+// counters n_pend / n_pqu / n_pqe were zeroed by the previous step's
 // finalisation.
-__global__ void k_col_round(KParams P, Dev d, int round) {
+#define CC_WAIT (1ull << 32)
+#define CC_REJ (1ull << 48)
+__global__ void k_col_resolve(KParams P, Dev d) {
   const uint32_t step = d.ctl->step;
-  const uint32_t rt = round_tag(step, round);
+  const uint32_t rt = round_tag(step, 0);
   __shared__ uint32_t pre[NSHARD + 1];
   const uint32_t n = sl_prefix(d.conf, pre);
-  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
-    const int2 e = sl_at(d.conf, pre, t);
-    if (conf_entry(d, e, step, rt)) d.pq_ent[wave_slot(&d.ctl->n_pqe)] = e;
-  }
-}
-
-__global__ void k_col_units(KParams P, Dev d, int round) {
-  const uint32_t step = d.ctl->step;
-  const uint32_t rt = round_tag(step, round);
-  __shared__ uint32_t pre[NSHARD + 1];
-  const uint32_t n = sl_prefix(d.plist, pre);
   int pend = 0;
   for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
-    const int u = sl_at(d.plist, pre, t).x;
-    if (conf_unit(d, u, step, rt)) {  // still pending: the tail's unit list
-      ++pend;
-      d.pq_units[wave_slot(&d.ctl->n_pqu)] = u;
+    const int2 e = sl_at(d.conf, pre, t);
+    const int u = e.x, kq = e.y & 0x7fffffff;
+    unsigned long long inc = 0;
+    if (state_of(d, u, step) == S_PEND) {
+      const uint32_t sk = state_of(d, kq, step);
+      if (sk == S_PEND) {
+        inc = CC_WAIT;
+        d.pq_ent[wave_slot(&d.ctl->n_pqe)] = e;
+      } else if ((sk == S_ACC) == (e.y < 0)) {
+        inc = CC_REJ;
+        mark_rej(d, u, (step & 0x3fffffffu) << 2);
+      }
+    }
+    const unsigned long long old = atomicAdd(&d.ccnt[u], inc - 1ull);
+    if ((uint32_t)old != 1u) continue;
+    // u's last entry: every other entry of u has made its change of the word
+    const unsigned long long now = old + inc - 1ull;
+    d.ccnt[u] = 0ull;
+    if ((now >> 48) == 0 && state_of(d, u, step) == S_PEND) {
+      if (now >> 32) {  // still pending: the tail's unit list, stamped for its round 1
+        ++pend;
+        d.pq_units[wave_slot(&d.ctl->n_pqu)] = u;
+      } else {
+        set_state(d, u, step, S_ACC);
+      }
     }
   }
   if (pend) atomicAdd(&d.ctl->n_pend, (uint32_t)pend);
 }
 
 // single workgroup: the remaining rounds on the compacted pending entries and
-// units (k_col_round, k_col_units), until nothing is pending
+// units (k_col_resolve), until nothing is pending
 __global__ void __launch_bounds__(1024) k_col_tail(KParams P, Dev d, int round0) {
   __shared__ uint32_t npend;
   if (d.ctl->n_pend == 0) return;
@@ -3419,13 +3467,13 @@ __device__ __forceinline__ void rej_copy(const KParams& P, const Dev& d, int m, 
 #ifndef REJ_UNROLL  // rejected units whose lookups a lane group has in flight at once
 #define REJ_UNROLL 1
 #endif
-__global__ void k_rej_commit(KParams P, Dev d) {
+// (workgroup blk of nblk taking part)
+__device__ __forceinline__ void rej_commit(const KParams& P, const Dev& d, uint32_t blk, uint32_t nblk) {
   const int NA = P.NA;
   __shared__ uint32_t pre[NSHARD + 1];
   const uint32_t n = sl_prefix(d.rej, pre);
   const int lane = threadIdx.x % REJ_LANES;
-  const uint32_t w0 = (blockIdx.x * blockDim.x + threadIdx.x) / REJ_LANES,
-                 nw = (gridDim.x * blockDim.x) / REJ_LANES;
+  const uint32_t w0 = (blk * blockDim.x + threadIdx.x) / REJ_LANES, nw = (nblk * blockDim.x) / REJ_LANES;
   constexpr int U = REJ_UNROLL;
   // REJ_UNROLL units per pass: each step of their lookup chains (unit ->
   // slot -> kind -> members) issued for all of them before the next, so a
@@ -3656,12 +3704,13 @@ __global__ void __launch_bounds__(256, PAIR_WAVES) k_pair_scan(KParams P, Dev d)
 // and cis gates (1954-1985 / 2009-2039) on each pair; a pair becomes an
 // accepting edge when its keyed draw is below the acceptance probability.
 // The greedy kernels below replay the reference's loop order on the edges.
-__global__ void k_rxn_exact(KParams P, Dev d) {
+// (workgroup blk of nblk taking part)
+__device__ __forceinline__ void rxn_exact(const KParams& P, const Dev& d, uint32_t blk, uint32_t nblk) {
   const int NA = P.NA, NB = P.NB;
   const uint32_t step = d.ctl->step;
   __shared__ uint32_t pre[NSHARD + 1];
   const uint32_t n = sl_prefix(d.pairs, pre);
-  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+  for (uint32_t t = blk * blockDim.x + threadIdx.x; t < n; t += nblk * blockDim.x) {
     const int2 pr = sl_at(d.pairs, pre, t);
     const int2 ra = d.rec[pr.x].id, rb = d.rec[pr.y].id;
     if (P.dbg_cand) atomicAdd(&d.ctl->rxn_kind[0], 1u);
@@ -3723,6 +3772,16 @@ __global__ void k_rxn_exact(KParams P, Dev d) {
   }
 }
 
+
+// The revert of the rejected units (workgroups [0, nrej)) beside the exact
+// reaction tests (the rest) in one launch: the tests read each record's final
+// position where it is (R of a rejected unit, which the revert copies into
+// R_new), so neither half waits for the other; both are done before k_match
+// snaps associated receptors in R_new.
+__global__ void k_commit_rxn(KParams P, Dev d, int nrej) {
+  if ((int)blockIdx.x < nrej) rej_commit(P, d, blockIdx.x, (uint32_t)nrej);
+  else rxn_exact(P, d, blockIdx.x - (uint32_t)nrej, gridDim.x - (uint32_t)nrej);
+}
 
 // ---------------------------------------------------------------- greedy
 // In-place bitonic sort of keys[0..np) (np a power of two) by one workgroup.
@@ -4098,6 +4157,19 @@ __global__ void __launch_bounds__(1024) k_finalize(KParams P, Dev d, double time
     atomicAdd(&tot[l], min(d.shard_cnt[k], cap));
     d.shard_cnt[k] = 0;
   }
+  // the next step's complexes: dissolve those whose bonds changed, or rebuild
+  // every one when the appended rows fill half of members[] or this step's
+  // dirty list overflowed (read by every thread before thread 0 writes them)
+  const uint32_t fstep = d.ctl->step;
+  const uint32_t ff = (d.ctl->cx_cursor > P.cx_limit || d.ctl->n_dirty[fstep & 1] > (uint32_t)P.N) ? 1u : 0u;
+  if (P.NB > 0) {
+    if (ff) {
+      cx_reset_all(P, d, threadIdx.x, blockDim.x);
+    } else {
+      cx_dissolve_dirty(P, d, fstep);
+      if (threadIdx.x == 0) d.ctl->full_now = 0;
+    }
+  }
   __syncthreads();
   if (threadIdx.x != 0) return;
   for (int w = 1; w < (int)(blockDim.x >> 6); ++w)
@@ -4124,11 +4196,7 @@ __global__ void __launch_bounds__(1024) k_finalize(KParams P, Dev d, double time
     c->err_step = step;
     c->err_first = c->err;
   }
-  // the next step's k_cx_kill: rebuild every complex when the appended rows
-  // fill half of members[] or this step's dirty list overflowed
-  const uint32_t ff = (c->cx_cursor > P.cx_limit || c->n_dirty[step & 1] > (uint32_t)P.N) ? 1u : 0u;
-  c->force_full = ff;
-  c->n_forced += ff;
+  c->n_forced += ff;  // (diagnostics: full rebuilds latched here)
   c->maxc = maxc;
   c->obs_idx = obs_idx + 1;
   c->step = step + 1;
@@ -4139,10 +4207,10 @@ __global__ void __launch_bounds__(1024) k_finalize(KParams P, Dev d, double time
   c->last[7] = n_ovf;
   c->last_outl = c->n_outl;
   c->n_overflow = 0;
-  c->n_dirty[(step + 1) & 1] = 0;  // consumed by this step's k_cx_kill; the next step's reactions fill it
+  c->n_dirty[(step + 1) & 1] = 0;  // consumed above; the next step's reactions fill it
   c->n_heavy = 0;
   c->n_pend = 0;
-  c->n_pqu = 0;  // filled by the next step's k_col_round / k_col_units
+  c->n_pqu = 0;  // filled by the next step's k_col_resolve
   c->n_pqe = 0;
   c->n_rl = 0;
   c->n_cisc = 0;

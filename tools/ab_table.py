@@ -5,7 +5,7 @@ import json
 import sys
 
 KS = ["k_cx_kill", "k_classify", "k_propose", "k_propose_free", "k_complex_heavy", "k_scan", "k_rec_scatter",
-      "k_pair_scan", "k_col_exact", "k_col_rounds", "k_commit", "k_rxn_exact", "k_match", "k_diss_observe"]
+      "k_pair_scan", "k_col_exact", "k_col_rounds", "k_commit_rxn", "k_match", "k_diss_observe"]
 print("variant".ljust(16), "ms/step fresh  " + " ".join(k[2:][:9].rjust(9) for k in KS))
 for f in sorted(glob.glob(sys.argv[1] + "/*.json")):
     try:

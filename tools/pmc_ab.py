@@ -25,7 +25,7 @@ import sys
 import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("k_propose_free", "k_pair_scan", "k_col_exact", "k_rej_commit", "k_rxn_exact", "k_complex_heavy",
+KERNELS = ("k_propose_free", "k_pair_scan", "k_col_exact", "k_commit_rxn", "k_complex_heavy",
            "k_move_members")
 
 
