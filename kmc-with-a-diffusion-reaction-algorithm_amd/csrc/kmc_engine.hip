@@ -921,7 +921,17 @@ static int launch_step(kmc_sim* s, bool re_sort) {
   // receptor in R_new, and a receptor of a rejected unit must be reverted
   // before that — DESIGN.md §8, the rejected REJ_SIDE variant)
   // the revert and the exact reaction tests (one launch, k_commit_rxn)
+#ifndef COMMIT_RXN  // (A/B builds: 0 = the revert, then the reaction tests, in two launches)
+#define COMMIT_RXN 1
+#endif
+#if COMMIT_RXN
   TIMED(KI_COMMIT, (k_commit_rxn<<<gX + (K.NA > 0 ? 1024 : 0), T, 0, st>>>(K, d, gX)));
+#else
+  TIMED(KI_COMMIT, {
+    k_commit_rxn<<<gX, T, 0, st>>>(K, d, gX);
+    if (K.NA > 0) k_commit_rxn<<<1024, T, 0, st>>>(K, d, 0);
+  });
+#endif
   if (K.NA > 0) TIMED(KI_MATCH, (k_match<<<1, 1024, 0, st>>>(K, d)));
   TIMED(KI_DISS_OBSERVE, {
     k_diss_observe<<<gN, T, 0, st>>>(K, d);

@@ -2578,7 +2578,7 @@ struct TileLds {
   float4 pos[TCAP];
   int2 id[TCAP];                   // {home position | the record's flags, owner key}
   uint16_t tag[TCAP];              // segment | column << 8 of each staged record's cell
-  int cstart[CFLAT_MAX];           // [seg][hw · SUBC + 1] flat, bins = (cell column, sub-column): record
+  alignas(16) int cstart[CFLAT_MAX];  // [seg][hw · SUBC + 1] flat, bins = (cell column, sub-column): record
                                    // counts, then the LDS index of each bin's first record; [seg][hw · SUBC]
                                    // = the segment's end
   union {
@@ -2611,15 +2611,40 @@ __device__ __forceinline__ int tile_global(const TileLds& T, int l) {
   return 2 * (x & RID_PID) + (x < 0 ? 1 : 0);
 }
 
+// Thread t's SCAN_PER consecutive bin counters a[SCAN_PER·t ..] (16-byte
+// aligned): with SCAN_PER = 4 one ds_read_b128 / ds_write_b128 per thread,
+// whose 16-lane groups cover the 64 banks once — element-wise, lanes SCAN_PER
+// words apart hit every bank SCAN_PER times (SQ_LDS_BANK_CONFLICT).
+__device__ __forceinline__ void scan_ld(const int* a, int t, int m, int* v) {
+  if (SCAN_PER == 4 && 4 * t + 3 < m) {
+    const int4 x = *reinterpret_cast<const int4*>(a + 4 * t);
+    v[0] = x.x;
+    v[1] = x.y;
+    v[2] = x.z;
+    v[3] = x.w;
+    return;
+  }
+#pragma unroll
+  for (int k = 0; k < SCAN_PER; ++k) v[k] = SCAN_PER * t + k < m ? a[SCAN_PER * t + k] : 0;
+}
+__device__ __forceinline__ void scan_st(int* a, int t, int m, const int* v) {
+  if (SCAN_PER == 4 && 4 * t + 3 < m) {
+    *reinterpret_cast<int4*>(a + 4 * t) = make_int4(v[0], v[1], v[2], v[3]);
+    return;
+  }
+#pragma unroll
+  for (int k = 0; k < SCAN_PER; ++k)
+    if (SCAN_PER * t + k < m) a[SCAN_PER * t + k] = v[k];
+}
+
 // exclusive prefix sum of a[0..m) in LDS by the whole workgroup (m <= SCAN_PER·blockDim)
 __device__ __forceinline__ int block_excl_scan(int* a, int m, int* wtot) {
   const int t = threadIdx.x, lane = __lane_id(), w = t >> 6, nw = blockDim.x >> 6;
-  int sum = 0;  // (each thread's own entries are read again below: no register array)
+  int v[SCAN_PER];
+  scan_ld(a, t, m, v);
+  int sum = 0;
 #pragma unroll
-  for (int k = 0; k < SCAN_PER; ++k) {
-    const int i = SCAN_PER * t + k;
-    sum += i < m ? a[i] : 0;
-  }
+  for (int k = 0; k < SCAN_PER; ++k) sum += v[k];
   int inc = sum;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -2636,13 +2661,11 @@ __device__ __forceinline__ int block_excl_scan(int* a, int m, int* wtot) {
   int run = base + inc - sum;
 #pragma unroll
   for (int k = 0; k < SCAN_PER; ++k) {
-    const int i = SCAN_PER * t + k;
-    if (i < m) {
-      const int x = a[i];
-      a[i] = run;
-      run += x;
-    }
+    const int x = v[k];
+    v[k] = run;
+    run += x;
   }
+  scan_st(a, t, m, v);
   __syncthreads();
   return tot;
 }
@@ -2861,18 +2884,18 @@ __device__ bool tile_load(const KParams& P, const Dev& d, const TileGeo& G, Tile
         if (cell[k] >= 0) place(k, atomicAdd(&T.cstart[cell[k] & 0xffff], 1), cell[k]);
     }
     __syncthreads();
+    // every counter one bin up: element i takes element i - 1 (the previous
+    // thread's last element from its lane, or from LDS for a wave's lane 0)
     int v[SCAN_PER];
+    const int t = (int)threadIdx.x;
+    scan_ld(T.cstart, t, nflat, v);
+    const int prev_lane = __shfl_up(v[SCAN_PER - 1], 1, 64);
+    const int prev = t == 0 ? 0 : (__lane_id() == 0 ? (SCAN_PER * t - 1 < nflat ? T.cstart[SCAN_PER * t - 1] : 0) : prev_lane);
 #pragma unroll
-    for (int k = 0; k < SCAN_PER; ++k) {
-      const int i = SCAN_PER * (int)threadIdx.x + k;
-      v[k] = i >= 1 && i < nflat ? T.cstart[i - 1] : 0;
-    }
+    for (int k = SCAN_PER - 1; k >= 1; --k) v[k] = v[k - 1];
+    v[0] = prev;
     __syncthreads();
-#pragma unroll
-    for (int k = 0; k < SCAN_PER; ++k) {
-      const int i = SCAN_PER * (int)threadIdx.x + k;
-      if (i < nflat) T.cstart[i] = v[k];
-    }
+    scan_st(T.cstart, t, nflat, v);
   }
   __syncthreads();
   S(d, 4);

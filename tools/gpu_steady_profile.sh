@@ -41,7 +41,7 @@ if [ "$pmc" = "sq" ] || [ "$pmc" = "all" ]; then
   run_pmc sq1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_WAIT_ANY SQ_WAVE_CYCLES
   run_pmc sq2 SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES
   run_pmc tcc TCC_HIT_sum TCC_MISS_sum
-  echo "k_bfs k_propose_free k_move_members k_cx_check k_complex_heavy k_rec_scatter k_pair_scan k_col_exact k_rej_commit k_rxn_exact k_match k_diss_observe" | \
+  echo "k_bfs k_propose_free k_move_members k_cx_check k_complex_heavy k_rec_scatter k_pair_scan k_col_exact k_col_resolve k_commit_rxn k_match k_diss_observe" | \
     python3 "$root/tools/pmc_summary.py" $(find "$out/sq1" "$out/sq2" "$out/tcc" -name '*counter_collection.csv') > "$out/pmc_summary.txt"
 fi
 rm -f $state
