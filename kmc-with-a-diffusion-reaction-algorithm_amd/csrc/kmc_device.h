@@ -27,6 +27,10 @@ struct KParams {
   double bond_cut, cis_cut, thetapd_cut, thetaot_cut, cis_theta_cut;
   // exact squared-distance thresholds: sqrt(s) < c  <=>  s < T(c)
   double T_aa, T_ab, T_bb, T_bond, T_cis;
+  // k_col_exact's refinement from the records (col_refine): squared float distances below which a
+  // ligand pair (2RB) / ligand–receptor pair (RA + RB + 0.3 Å) may collide, + 2.5 Å for the rounding
+  float ref_bb, ref_ab;
+  int col_refine;  // 1 (default; KMC_COL_REFINE=0 turns it off: the same results, more fp64 gathers)
   kmcr::Key key;
   int tcap;  // LDS tile record capacity (<= TCAP; lowered only to test the global path)
   int tile;  // cells per tile side of the LDS scans (<= TILE_MAX)

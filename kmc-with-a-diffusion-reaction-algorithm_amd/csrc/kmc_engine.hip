@@ -312,6 +312,12 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   K.T_bb = sqrt_threshold(p->rb_radius + p->rb_radius);
   K.T_bond = sqrt_threshold(p->bond_dist_cutoff);
   K.T_cis = sqrt_threshold(p->cis_dist_cutoff);
+  K.ref_bb = (float)((2 * p->rb_radius + 2.5) * (2 * p->rb_radius + 2.5));
+  K.ref_ab = (float)((p->ra_radius + p->rb_radius + 0.3 + 2.5) * (p->ra_radius + p->rb_radius + 0.3 + 2.5));
+  {
+    const char* cr = getenv("KMC_COL_REFINE");
+    K.col_refine = !(cr && *cr == '0');
+  }
   K.key = kmcr::make_key(p->seed, p->replica);
 
   s->ncell = 2 * K.ncx * K.ncy;  // (row, kind, column) record cells
@@ -844,6 +850,9 @@ static int debug_check_lists(kmc_sim* s) {
   return KMC_OK;
 }
 
+#ifndef COARSE_N  // proteins from which the per-slot passes take 4 slots per thread
+#define COARSE_N (4 << 20)
+#endif
 // s->tnow (this step bracketed) is set by the caller
 static int launch_step(kmc_sim* s, bool re_sort) {
   const KParams& K = s->K;
@@ -868,7 +877,10 @@ static int launch_step(kmc_sim* s, bool re_sort) {
   if (K.NB > 0 && (s->need_full || re_sort || s->always_full))
     TIMED(KI_CX_KILL, (k_cx_kill<<<std::min(gN, 1024), T, 0, st>>>(K, d)));
   s->need_full = false;
-  TIMED(KI_CLASSIFY, (k_classify<<<gN, T, 0, st>>>(K, d)));
+  // slots per thread of the per-slot passes k_classify / k_diss_observe
+  const int per = K.N >= COARSE_N ? 4 : 1, gP = (K.N + T * per - 1) / (T * per);
+  if (per == 4) TIMED(KI_CLASSIFY, (k_classify<4><<<gP, T, 0, st>>>(K, d)));
+  else TIMED(KI_CLASSIFY, (k_classify<1><<<gP, T, 0, st>>>(K, d)));
   // KI_PROPOSE brackets the whole proposal phase: every protein's R read and
   // R_new written once (the bench's roofline unit).  Complexes kept or newly
   // registered (k_bfs); their rigid-move parameters (cx_params, in the first
@@ -896,7 +908,7 @@ static int launch_step(kmc_sim* s, bool re_sort) {
   const int gX = std::min(2048, (K.N + T - 1) / T);  // grid-stride kernels over device-sized lists
   const int ntiles = s->ntiles;
   // collision candidates and reaction candidates, one staging of each tile
-  TIMED(KI_PAIR_SCAN, (k_pair_scan<<<ntiles, 256, 0, st>>>(K, d)));
+  TIMED(KI_PAIR_SCAN, (k_pair_scan<<<ntiles, PAIR_THREADS, 0, st>>>(K, d)));
   // the tiles too dense for the pair scan's LDS, one per workgroup, then the
   // exact tests of the candidates
   TIMED(KI_COL_EXACT, {
@@ -934,8 +946,9 @@ static int launch_step(kmc_sim* s, bool re_sort) {
 #endif
   if (K.NA > 0) TIMED(KI_MATCH, (k_match<<<1, 1024, 0, st>>>(K, d)));
   TIMED(KI_DISS_OBSERVE, {
-    k_diss_observe<<<gN, T, 0, st>>>(K, d);
-    k_finalize<<<1, 1024, 0, st>>>(K, d, s->p.time_step, gN);
+    if (per == 4) k_diss_observe<4><<<gP, T, 0, st>>>(K, d);
+    else k_diss_observe<1><<<gP, T, 0, st>>>(K, d);
+    k_finalize<<<1, 1024, 0, st>>>(K, d, s->p.time_step, gP);
   });
   if (s->tnow) s->tslot = (s->tslot + 1) % TRING;
   // R_new becomes R (main.cpp:2164-2191): swap the bead buffers

@@ -63,7 +63,7 @@ struct Dev {
   double* cxp;       // [NB][16] rigid-move parameters of the complex rooted at lb (cx_params)
   uint32_t* shuf_tag;  // [NB] step whose shuffled row of root lb is in shuf
   uint32_t mcap;     // members[] capacity (3N): rows are appended until a full rebuild
-  int32_t* croot;    // [N] slot of the root ligand of the protein's registered complex, -1 none
+  int32_t* croot;    // [N] slot of the root ligand of the protein's registered complex | CROOT_BIG, -1 none
   uint32_t* cx_alive;  // [NB] 1 while ligand lb roots a registered complex
   uint32_t* bfs_cand;  // [NB] step tag: ligand lb runs the BFS this step
   int32_t* dlist;    // [2][N] proteins whose bonds changed during step s (list s & 1)
@@ -117,9 +117,10 @@ struct Dev {
 
 // one record (32 B): float reference point, ids, cis site
 struct alignas(16) Rec {
-  float4 pos;   // x, y of bead [1][1]; z span (receptor: lowest/highest domain; ligand: centre)
+  float4 pos;   // x, y of bead [1][1]; z span (receptor: lowest/highest domain; ligand: centre, then
+                // the first word of its subunit offsets, lig_pack)
   int2 id;      // {slot | cell code << 25 | st3 << 29 | st2 << 30 | isnew << 31, owner key}
-  float2 site;  // receptor [3][3] site xy (reaction prefilter); 0 for ligands
+  float2 site;  // receptor [3][3] site xy (reaction prefilter); ligand: the other two words of lig_pack
 };
 #define RID_PID 0x00ffffff  // the slot (global records) or the home position (the pair scan's LDS copies)
 #define RID_LIG (1 << 24)   // a ligand's record
@@ -179,6 +180,7 @@ __device__ __forceinline__ int cell_y(const KParams& P, double y) {
   return c < 0 ? 0 : (c >= P.ncy ? P.ncy - 1 : c);
 }
 
+#define CROOT_BIG (1 << 30)  // croot flag: the complex has more than CXL members (global-memory path)
 #define CXL 16  // members of a complex moved by the streamed path and staged in LDS by k_complex_heavy
 
 // slot for each calling lane (call from the lanes that emit)
@@ -214,40 +216,64 @@ __device__ __forceinline__ uint32_t wave_alloc(uint32_t* ctr, uint32_t qn) {
 // ================================================================ 1. classify
 // Unit kinds, main.cpp:584 (free receptor), 682-686 (cis dimer, moved at the
 // lower index), 905 (single ligand = BFS component of size 1).
+// CLASSIFY_PER slots per thread (their first loads issued together; chosen as
+// k_diss_observe's count)
+template <int CLASSIFY_PER>
 __global__ void k_classify(KParams P, Dev d) {
   const int NA = P.NA, NB = P.NB;
-  int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= P.N) return;
-  uint8_t kind = U_NONE;
-  int own = -1;
-  if (p < NA) {
-    int i = p;
-    int n2 = A_NEI2(d, i), n3 = A_NEI3(d, i);
-    if (A_ST2(d, i) == 0 && A_ST3(d, i) == 0) {
-      kind = U_FREE_A;
-      own = p;
-    } else if (n2 == 0 && n3 != 0 && A_NEI3(d, n3 - 1) == i + 1 && A_NEI2(d, n3 - 1) == 0) {
-      int q = n3 - 1;
-      const bool lead = d.id_of[i] < d.id_of[q];  // moved at the lower reference index
-      own = lead ? i : q;
-      kind = lead ? U_DIMER : U_DIMER_P;
+  const int p0 = blockIdx.x * blockDim.x * CLASSIFY_PER + threadIdx.x;
+  // the links / statuses and complex root of every slot of this thread first
+  int n2[CLASSIFY_PER], n3[CLASSIFY_PER], s2[CLASSIFY_PER], r[CLASSIFY_PER];
+#pragma unroll
+  for (int k = 0; k < CLASSIFY_PER; ++k) {
+    const int p = p0 + k * (int)blockDim.x;
+    n2[k] = n3[k] = s2[k] = 0;
+    r[k] = -1;
+    if (p >= P.N) continue;
+    if (p < NA) {
+      n2[k] = A_NEI2(d, p);
+      n3[k] = A_NEI3(d, p);
+      s2[k] = A_ST2(d, p) | A_ST3(d, p);
+    } else {
+      const int b = p - NA;
+      n2[k] = B_NEI(d, b, 2);
+      n3[k] = B_NEI(d, b, 3);
+      s2[k] = B_NEI(d, b, 4);
     }
-  } else {
-    int b = p - NA;
-    if (B_NEI(d, b, 2) == 0 && B_NEI(d, b, 3) == 0 && B_NEI(d, b, 4) == 0) {
+    r[k] = d.croot[p];
+    if (r[k] >= 0) r[k] &= ~CROOT_BIG;
+  }
+#pragma unroll
+  for (int k = 0; k < CLASSIFY_PER; ++k) {
+    const int p = p0 + k * (int)blockDim.x;
+    if (p >= P.N) continue;
+    uint8_t kind = U_NONE;
+    int own = -1;
+    if (p < NA) {
+      const int i = p;
+      if (s2[k] == 0) {
+        kind = U_FREE_A;
+        own = p;
+      } else if (n2[k] == 0 && n3[k] != 0 && A_NEI3(d, n3[k] - 1) == i + 1 && A_NEI2(d, n3[k] - 1) == 0) {
+        int q = n3[k] - 1;
+        const bool lead = d.id_of[i] < d.id_of[q];  // moved at the lower reference index
+        own = lead ? i : q;
+        kind = lead ? U_DIMER : U_DIMER_P;
+      }
+    } else if (n2[k] == 0 && n3[k] == 0 && s2[k] == 0) {
       kind = U_FREE_B;
       own = p;
     }
+    // a member of a complex registered in an earlier step and untouched since
+    // (dissolved otherwise): its unit is that complex (new ones are registered
+    // by k_bfs)
+    if (r[k] >= 0) {
+      own = r[k];
+      if (r[k] == p) kind = U_COMPLEX;
+    }
+    d.ukind[p] = kind;
+    d.owner[p] = own < 0 ? -1 : d.id_of[own];  // -1: member of a complex k_bfs registers this step
   }
-  // a member of a complex registered in an earlier step and untouched since
-  // (k_cx_kill): its unit is that complex (new ones are registered by k_bfs)
-  const int r = d.croot[p];
-  if (r >= 0) {
-    own = r;
-    if (r == p) kind = U_COMPLEX;
-  }
-  d.ukind[p] = kind;
-  d.owner[p] = own < 0 ? -1 : d.id_of[own];  // -1: member of a complex k_bfs registers this step
 }
 
 // Complexes are kept from step to step: a BFS row depends only on the bond
@@ -281,7 +307,7 @@ __device__ __forceinline__ void cx_dissolve_dirty(const KParams& P, const Dev& d
   for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) {
     const int p = d.dlist[(size_t)li * P.N + t];
     if (p >= NA) d.bfs_cand[p - NA] = next;
-    const int r = d.croot[p];
+    const int r = d.croot[p] & ~CROOT_BIG;
     if (r < 0 || atomicExch(&d.cx_alive[r - NA], 0u) != 1u) continue;
     const int b = r - NA, off = d.cx_off[b], sz = d.cx_size[b];
     for (int i = 0; i < sz; ++i) {
@@ -355,7 +381,7 @@ __device__ __forceinline__ void register_complex(const KParams& P, const Dev& d,
     int m = q[t * STRIDE];
     d.members[off + t] = m;
     d.owner[m] = rootid;
-    d.croot[m] = p;
+    d.croot[m] = p | (qn > CXL ? CROOT_BIG : 0);
     nb += m >= NA;
   }
   d.cx_alive[p - NA] = 1;
@@ -605,8 +631,8 @@ __device__ __forceinline__ void tile_bucket_push(const KParams& P, const Dev& d,
     }
 }
 
-__device__ __forceinline__ void put_rec(const KParams& P, const Dev& d, uint2 h, int p, int w, int st, int own,
-                                        double x, double y, double zlo, double zhi, double sx, double sy) {
+__device__ __forceinline__ void put_rec_raw(const KParams& P, const Dev& d, uint2 h, int p, int w, int st, int own,
+                                            double x, double y, float4 pos, float2 site) {
   const int cx = cell_x(P, x), cy = cell_y(P, y);
   const int dx = cx - (int)(h.y & 0xffffu), dy = cy - (int)(h.y >> 16);
   const int ri = 2 * (int)h.x + w;
@@ -620,11 +646,44 @@ __device__ __forceinline__ void put_rec(const KParams& P, const Dev& d, uint2 h,
     tile_bucket_push(P, d, ri, cx, cy);
   }
   Rec r;
-  r.pos = make_float4((float)x, (float)y, (float)zlo, (float)zhi);
+  r.pos = pos;
   r.id = make_int2(p | (p >= P.NA ? RID_LIG : 0) | code << RID_CODE_SHIFT | st | (w << 31), own);
-  r.site = make_float2((float)sx, (float)sy);
+  r.site = site;
   d.rec[ri] = r;
   if (P.dbg_recs) d.rec_step[ri] = d.ctl->step;
+}
+// a receptor's record: reference point [1][1] xy, z span of its domains, [3][3] site
+__device__ __forceinline__ void put_rec(const KParams& P, const Dev& d, uint2 h, int p, int w, int st, int own,
+                                        double x, double y, double zlo, double zhi, double sx, double sy) {
+  put_rec_raw(P, d, h, p, w, st, own, x, y, make_float4((float)x, (float)y, (float)zlo, (float)zhi),
+              make_float2((float)sx, (float)sy));
+}
+// A ligand's record: centre [1][1] and the offsets of its three subunit
+// centres [j][1] (j = 2..4) from it, rounded to whole Å (9 signed bytes in the
+// words a receptor record uses for its z top and site).  k_col_exact tests a
+// candidate pair's subunits from the records first (col_refine) and gathers
+// the fp64 beads only when that cannot rule the collision out.  Byte 9 set:
+// an offset out of the byte range (no such ligand within the extent bound),
+// the pair goes to the exact test.
+__device__ __forceinline__ uint32_t q8(double v, uint32_t& big) {
+  const double r = rint(v);
+  big |= (r > 120.0 || r < -120.0) ? 1u : 0u;
+  return (uint32_t)((int)fmin(fmax(r, -120.0), 120.0) & 0xff);
+}
+__device__ __forceinline__ void put_rec_lig(const KParams& P, const Dev& d, uint2 h, int p, int w, int own, double cx,
+                                            double cy, double cz, const double* sx, const double* sy,
+                                            const double* sz) {
+  uint32_t big = 0, b[9];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    b[3 * j] = q8(sx[j] - cx, big);
+    b[3 * j + 1] = q8(sy[j] - cy, big);
+    b[3 * j + 2] = q8(sz[j] - cz, big);
+  }
+  const uint32_t w0 = b[0] | b[1] << 8 | b[2] << 16 | b[3] << 24, w1 = b[4] | b[5] << 8 | b[6] << 16 | b[7] << 24,
+                 w2 = b[8] | big << 8;
+  put_rec_raw(P, d, h, p, w, 0, own, cx, cy, make_float4((float)cx, (float)cy, (float)cz, __uint_as_float(w0)),
+              make_float2(__uint_as_float(w1), __uint_as_float(w2)));
 }
 
 // debug (KMC_DEBUG_RECS=1), after the proposal phase: every protein's two
@@ -654,6 +713,16 @@ __device__ __forceinline__ void put_rec_glb(const KParams& P, const Dev& d, uint
     const double2 s33 = B.Axy(p, 3, 3);
     sx = s33.x;
     sy = s33.y;
+  } else {
+    double ux[3], uy[3], uz[3];
+    for (int j = 0; j < 3; ++j) {
+      const double2 xy = B.Bxy(p - P.NA, j + 2, 1);
+      ux[j] = xy.x;
+      uy[j] = xy.y;
+      uz[j] = B.B(p - P.NA, j + 2, 1, 2);
+    }
+    put_rec_lig(P, d, h, p, w, own, x, y, zl, ux, uy, uz);
+    return;
   }
   put_rec(P, d, h, p, w, st, own, x, y, zl, zh, sx, sy);
 }
@@ -1044,8 +1113,13 @@ __device__ void propose_free_b(const KParams& P, const Dev& d, int lb, int p, ui
   }
   if (!ext) atomicOr(&d.ctl->err, ERR_GEOMETRY);
   // records: the centre [1][1] (a free ligand is its own unit)
-  put_rec(P, d, h, p, 0, 0, (int)rp, r[0][0][0], r[0][0][1], r[0][0][2], r[0][0][2], 0.0, 0.0);
-  put_rec(P, d, h, p, 1, 0, (int)rp, scx[0], scy[0], nzs[0][0], nzs[0][0], 0.0, 0.0);
+  {
+    const double ox3[3] = {r[1][0][0], r[2][0][0], r[3][0][0]}, oy3[3] = {r[1][0][1], r[2][0][1], r[3][0][1]},
+                 oz3[3] = {r[1][0][2], r[2][0][2], r[3][0][2]};
+    put_rec_lig(P, d, h, p, 0, (int)rp, r[0][0][0], r[0][0][1], r[0][0][2], ox3, oy3, oz3);
+    const double nz3[3] = {nzs[1][0], nzs[2][0], nzs[3][0]};
+    put_rec_lig(P, d, h, p, 1, (int)rp, scx[0], scy[0], nzs[0][0], scx + 1, scy + 1, nz3);
+  }
 }
 
 // ---------------------------------------------------------------- stamps
@@ -1793,7 +1867,13 @@ __device__ __forceinline__ void cx_put_new(const KParams& P, const Dev& d, CxLds
   // reference point (ref_point): [1][1] xy; z span of the domain centres
   // [j][1] (receptor) or the centre's z (ligand); receptor [3][3] site
   double zl = b[2], zh = b[2], sx = 0.0, sy = 0.0;
-  if (!kind) {
+  if (kind) {
+    const double ux[3] = {b[2 * 3], b[4 * 3], b[6 * 3]}, uy[3] = {b[2 * 3 + 1], b[4 * 3 + 1], b[6 * 3 + 1]},
+                 uz[3] = {b[2 * 3 + 2], b[4 * 3 + 2], b[6 * 3 + 2]};
+    put_rec_lig(P, d, home, m, 1, own, b[0], b[1], b[2], ux, uy, uz);
+    return;
+  }
+  {
     const double z1 = b[2], z2 = b[(4) * 3 + 2], z3 = b[(8) * 3 + 2], z4 = b[(12) * 3 + 2];
     zl = fmin(fmin(z1, z2), fmin(z3, z4));
     zh = fmax(fmax(z1, z2), fmax(z3, z4));
@@ -2052,8 +2132,12 @@ __device__ __forceinline__ void move_member(const KParams& P, const Dev& d, int 
     if constexpr (IS_A)
       put_rec(P, d, h, p, w, st, own, r[0].x, r[0].y, fmin(fmin(r[16].x, r[16].y), fmin(r[20].x, r[20].y)),
               fmax(fmax(r[16].x, r[16].y), fmax(r[20].x, r[20].y)), r[10].x, r[10].y);
-    else
-      put_rec(P, d, h, p, w, st, own, r[0].x, r[0].y, r[8].x, r[8].x, 0.0, 0.0);
+    else {
+      // subunit centres [j][1]: xy rows 2, 4, 6; z of [2][1] in row 8 (.y), of [3][1], [4][1] in row 10
+      const double ux[3] = {r[2].x, r[4].x, r[6].x}, uy[3] = {r[2].y, r[4].y, r[6].y},
+                   uz[3] = {r[8].y, r[10].x, r[10].y};
+      put_rec_lig(P, d, h, p, w, own, r[0].x, r[0].y, r[8].x, ux, uy, uz);
+    }
   };
   recs(0);
   // beads (j, k) and (j+1, k), j odd: xy rows (j-1)·NK + (k-1) and j·NK + (k-1),
@@ -2258,7 +2342,7 @@ __global__ void __launch_bounds__(256, MEMBER_WAVES) k_move_members(KParams P, D
   const int p = blockIdx.x * blockDim.x + threadIdx.x, NA = P.NA;
   if (p >= P.N) return;
   const int r = d.croot[p];
-  if (r < 0 || d.cx_size[r - NA] > CXL) return;
+  if (r < 0 || (r & CROOT_BIG)) return;  // (the flag: no cx_size load on the member's chain)
   const double* cp = d.cxp + (size_t)(r - NA) * CXP;
   if (p < NA) move_member<true>(P, d, p, cp, r);
   else move_member<false>(P, d, p - NA, cp, r);
@@ -2962,6 +3046,7 @@ __device__ __forceinline__ void item_ranges(const KParams& P, const TileLds& T, 
 // (16 records = 128 B apart mod 256 B).  Records base + 4·lane + wv (the
 // round-robin order before) put a group's lanes 64 B apart: 4-way conflicts
 // on every owner read (SQ_LDS_BANK_CONFLICT, profiles/r05/ab_walk).
+#define PAIR_THREADS 256  // threads of a k_pair_scan workgroup (tile_walk's wave count)
 __device__ __forceinline__ int walk_item(int base, int lane, int wv, int nw) {
 #if WALK_PERM
   if (nw == 4) return base + 16 * ((5 * (lane >> 4) + 4 * wv) & 15) + (lane & 15);
@@ -2975,7 +3060,8 @@ __device__ __forceinline__ void tile_walk(const TileGeo& G, const TileLds& T, ui
   // records are in bin order, so each wave samples the whole block and the
   // waves of a workgroup walk about the same number of pairs
 #if WALK_STRIDE
-  const int nw = blockDim.x >> 6, wv = threadIdx.x >> 6;
+  constexpr int nw = PAIR_THREADS / 64;  // (the pair scan's only block size)
+  const int wv = threadIdx.x >> 6;
 #endif
   for (int base = 0; base < n; base += blockDim.x) {
 #if WALK_STRIDE
@@ -3208,12 +3294,66 @@ __device__ __forceinline__ void mark_rej(const Dev& d, int u, uint32_t tag) {
 // (own unit, or a later unit's old position) rejects u outright; one with an
 // earlier unit's record becomes a conflict entry (u, kq, isnew) for pass C.
 // Unit states this step: untouched = accepted, S_PEND, S_REJ (atomicMax).
-// one candidate (proposal record a, record b)
-__device__ __forceinline__ void col_exact_one(const KParams& P, const Dev& d, int2 a, int2 b, uint32_t tag) {
+// Refinement from the two records alone (float, conservative): can the pair
+// collide?  A ligand record carries its subunit centres to within 0.87 Å
+// (lig_pack); a receptor's domain centres lie within 0.3 Å of the vertical
+// segment (record x, y; z from its lowest to its highest domain) — both
+// enforced by the extent bound.  Ligand pairs: some subunit pair within 2RB,
+// ligand–receptor: some subunit within RA + RB of the segment, each with the
+// rounding margins in P.ref_bb / P.ref_ab.  Receptor pairs pass (their
+// prefilter is already the exact test's up to 2 Å).  At C5, 93 % of the
+// ligand candidates do not collide (KMC_DEBUG_CAND).
+__device__ __forceinline__ void lig_subs(const Rec& r, float* x, float* y, float* z, bool& ok) {
+  const uint32_t w0 = __float_as_uint(r.pos.w), w1 = __float_as_uint(r.site.x), w2 = __float_as_uint(r.site.y);
+  const uint32_t b[9] = {w0, w0 >> 8, w0 >> 16, w0 >> 24, w1, w1 >> 8, w1 >> 16, w1 >> 24, w2};
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    x[j] = r.pos.x + (float)(int8_t)(b[3 * j] & 0xff);
+    y[j] = r.pos.y + (float)(int8_t)(b[3 * j + 1] & 0xff);
+    z[j] = r.pos.z + (float)(int8_t)(b[3 * j + 2] & 0xff);
+  }
+  ok = ((w2 >> 8) & 1u) == 0u;
+}
+__device__ __forceinline__ bool col_refine(const KParams& P, const Rec& a, const Rec& b) {
+  const bool la = (a.id.x & RID_LIG) != 0, lb = (b.id.x & RID_LIG) != 0;
+  if (!la && !lb) return true;
+  float ax[3], ay[3], az[3];
+  bool ok;
+  lig_subs(la ? a : b, ax, ay, az, ok);
+  bool may = !ok;
+  if (la && lb) {
+    float bx[3], by[3], bz[3];
+    bool okb;
+    lig_subs(b, bx, by, bz, okb);
+    may |= !okb;
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const float dx = ax[j] - bx[k], dy = ay[j] - by[k], dz = az[j] - bz[k];
+        may |= dx * dx + dy * dy + dz * dz < P.ref_bb;
+      }
+    return may;
+  }
+  const Rec& R = la ? b : a;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const float dx = ax[j] - R.pos.x, dy = ay[j] - R.pos.y;
+    const float dz = fmaxf(fmaxf(R.pos.z - az[j], az[j] - R.pos.w), 0.0f);
+    may |= dx * dx + dy * dy + dz * dz < P.ref_ab;
+  }
+  return may;
+}
+
+// one candidate (proposal record A, record B)
+__device__ __forceinline__ void col_exact_one(const KParams& P, const Dev& d, const Rec& A, const Rec& B, uint32_t tag) {
+  const int2 a = A.id, b = B.id;
   int m = a.x & RID_PID, u = a.y, q = b.x & RID_PID, kq = b.y;
   bool isnew = b.x < 0;
   bool hit;
-  if (COL_AA_FAST && m < P.NA && q < P.NA) {
+  if (P.col_refine && !col_refine(P, A, B)) {
+    hit = false;
+  } else if (COL_AA_FAST && m < P.NA && q < P.NA) {
     // receptor against receptor: domain [1][1] against domain [1][1] only
     // (exact_collide's first case), two rows of each instead of load_own's six
     const Beads& Q = isnew ? d.nxt : d.cur;
@@ -3318,7 +3458,7 @@ void dense_block(const KParams& P, const Dev& d, int4 blk, uint32_t tag) {
       const Rec o = d.rec[rn];
       if (prop && col_pair(me, mr.pos, o.id, o.pos)) {
         if (o.id.y < 0) atomicOr(&d.ctl->err, ERR_RESOLVE);
-        else col_exact_one(P, d, me, o.id, tag);
+        else col_exact_one(P, d, mr, o, tag);
       }
       if (rx && rxn_pair(me, mr.pos, mr.site, o.id, o.pos, o.site)) sl_push(d.pairs, make_int2(ri, rn), &d.ctl->err);
     });
@@ -3348,7 +3488,18 @@ __global__ void k_col_exact(KParams P, Dev d) {
   const uint32_t n = sl_prefix(d.cand, pre);
   for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
     const int2 c = sl_at(d.cand, pre, t);
-    col_exact_one(P, d, d.rec[c.x].id, d.rec[c.y].id, tag);
+    // the ids first; the rest of the two records (same lines) only for a
+    // pair with a ligand, which col_refine reads
+    Rec A, B;
+    A.id = d.rec[c.x].id;
+    B.id = d.rec[c.y].id;
+    if ((A.id.x | B.id.x) & RID_LIG) {
+      A.pos = d.rec[c.x].pos;
+      A.site = d.rec[c.x].site;
+      B.pos = d.rec[c.y].pos;
+      B.site = d.rec[c.y].site;
+    }
+    col_exact_one(P, d, A, B, tag);
   }
 }
 
@@ -3689,7 +3840,7 @@ __device__ __forceinline__ bool pair_scan_block(const KParams& P, const Dev& d, 
 #ifndef PAIR_WAVES  // minimum waves per SIMD of the pair scan (A/B builds: tools/build_variants.py)
 #define PAIR_WAVES 5
 #endif
-__global__ void __launch_bounds__(256, PAIR_WAVES) k_pair_scan(KParams P, Dev d) {
+__global__ void __launch_bounds__(PAIR_THREADS, PAIR_WAVES) k_pair_scan(KParams P, Dev d) {
   __shared__ TileLds T;
   __shared__ float2 site[TCAP];
   WgList& Lc = T.u.l.Lc;
@@ -4090,49 +4241,75 @@ __device__ __forceinline__ int wave_max(int v) {
 // its final value is a function of the receptor's own draw, so the partner's
 // value read before or after its own update gives the same answer); it then
 // counts its final bonds.  Ligand: cluster statistics of this step's BFS.
+// DISS_PER proteins per thread (their first loads issued together): 4 for the
+// large systems (C5: 101 -> 61 us), 1 below 4M proteins, where fewer
+// workgroups than the CUs' slots would cost more than the overlap gains (C3:
+// 22 -> 25 us with 4)
+template <int DISS_PER>
 __global__ void __launch_bounds__(256) k_diss_observe(KParams P, Dev d) {
   const int NA = P.NA, NB = P.NB;
   __shared__ int red[4][6];
-  int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t step = d.ctl->step;
   int v[6] = {0, 0, 0, 0, 0, 0};  // rl mono cis tot_prot tot_clu max
-  if (p < NA) {
-    const int i = p;
-    const uint32_t step = d.ctl->step;
-    int st2_i = A_ST2(d, i);
-    if (st2_i == 1 && rl_breaks(P, d, i, step)) {
-      int q = A_NEI2(d, i) - 1, k = A_NEI4(d, i);
-      int lb = q - NA;
-      A_ST2(d, i) = 0;
-      B_ST(d, lb, k) = 0;
-      A_NEI2(d, i) = 0;
-      A_NEI4(d, i) = 0;
-      B_NEI(d, lb, k) = 0;
-      mark_bond_change(P, d, i, step);
-      mark_bond_change(P, d, q, step);
-      st2_i = 0;
+  // DISS_PER proteins per thread, blockDim apart (each load coalesced): the
+  // status words / unit kinds of all of them in flight before the first branch
+  const int p0 = blockIdx.x * blockDim.x * DISS_PER + threadIdx.x;
+  int st2[DISS_PER], st3[DISS_PER];
+  uint8_t kind[DISS_PER];
+#pragma unroll
+  for (int k = 0; k < DISS_PER; ++k) {
+    const int p = p0 + k * (int)blockDim.x;
+    st2[k] = 0;
+    st3[k] = 0;
+    kind[k] = U_NONE;
+    if (p < NA) {
+      st2[k] = A_ST2(d, p);
+      st3[k] = A_ST3(d, p);
+    } else if (p < P.N) {
+      kind[k] = d.ukind[p];
     }
-    // a decomposed trajectory counts the bonds of the receptors its slab owns,
-    // a cis pair at the owner of its lower reference index (dd_owned)
-    v[0] = dd_owned(P, d, d.id_of[i]) ? st2_i : 0;
-    if (A_ST3(d, i) == 1) {
-      int q = A_NEI3(d, i) - 1;
-      if (i < q) {
-        int st2_q = A_ST2(d, q);
-        if (st2_q == 1 && rl_breaks(P, d, q, step)) st2_q = 0;
-        const bool mono = st2_i == 0 && st2_q == 0;
-        if (!cis_diss(P, d, i, q, mono, step)) v[mono ? 1 : 2] = dd_owned(P, d, min(d.id_of[i], d.id_of[q])) ? 1 : 0;
+  }
+#pragma unroll
+  for (int k = 0; k < DISS_PER; ++k) {
+    const int p = p0 + k * (int)blockDim.x;
+    if (p < NA) {
+      const int i = p;
+      int st2_i = st2[k];
+      if (st2_i == 1 && rl_breaks(P, d, i, step)) {
+        int q = A_NEI2(d, i) - 1, kk = A_NEI4(d, i);
+        int lb = q - NA;
+        A_ST2(d, i) = 0;
+        B_ST(d, lb, kk) = 0;
+        A_NEI2(d, i) = 0;
+        A_NEI4(d, i) = 0;
+        B_NEI(d, lb, kk) = 0;
+        mark_bond_change(P, d, i, step);
+        mark_bond_change(P, d, q, step);
+        st2_i = 0;
       }
-    }
-  } else if (p < P.N) {
-    uint8_t k = d.ukind[p];
-    if (!dd_owned(P, d, d.id_of[p])) k = U_NONE;  // a unit (root ligand) of another slab
-    if (k == U_COMPLEX) {
-      int s = d.cx_size[p - NA];
-      v[3] = s;
-      v[4] = 1;
-      v[5] = s;
-    } else if (k == U_FREE_B) {
-      v[5] = 1;
+      // a decomposed trajectory counts the bonds of the receptors its slab owns,
+      // a cis pair at the owner of its lower reference index (dd_owned)
+      v[0] += dd_owned(P, d, d.id_of[i]) ? st2_i : 0;
+      if (st3[k] == 1) {
+        int q = A_NEI3(d, i) - 1;
+        if (i < q) {
+          int st2_q = A_ST2(d, q);
+          if (st2_q == 1 && rl_breaks(P, d, q, step)) st2_q = 0;
+          const bool mono = st2_i == 0 && st2_q == 0;
+          if (!cis_diss(P, d, i, q, mono, step)) v[mono ? 1 : 2] += dd_owned(P, d, min(d.id_of[i], d.id_of[q])) ? 1 : 0;
+        }
+      }
+    } else if (p < P.N) {
+      uint8_t kd = kind[k];
+      if (!dd_owned(P, d, d.id_of[p])) kd = U_NONE;  // a unit (root ligand) of another slab
+      if (kd == U_COMPLEX) {
+        int sz = d.cx_size[p - NA];
+        v[3] += sz;
+        v[4] += 1;
+        v[5] = max(v[5], sz);
+      } else if (kd == U_FREE_B) {
+        v[5] = max(v[5], 1);
+      }
     }
   }
   for (int f = 0; f < 5; ++f) v[f] = wave_sum(v[f]);
