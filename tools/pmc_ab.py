@@ -15,6 +15,7 @@ a table on stdout (ms/step, the pair scan and the selected kernels' counters).
 """
 from __future__ import annotations
 
+import re
 import argparse
 import csv
 import glob
@@ -57,7 +58,7 @@ def counters(path_glob):
     acc = {}
     for path in glob.glob(path_glob, recursive=True):
         for r in csv.DictReader(open(path)):
-            k = r["Kernel_Name"].split("(")[0].replace("kmcd::", "")
+            k = re.sub(r"^void (k_\w+)<\d+>$", r"\1", r["Kernel_Name"].split("(")[0].replace("kmcd::", ""))
             acc.setdefault(k, {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
 

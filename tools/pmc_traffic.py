@@ -8,6 +8,7 @@ wide coalesced streaming read, so it is doubled; WRITE_SIZE is taken as is.
 The first `skip` dispatches of every kernel (clock ramp) are dropped.
 Output: {kernel: {"fetch_bytes", "write_bytes", "traffic_bytes", "launches"}}.
 """
+import re
 import collections
 import csv
 import json
@@ -19,7 +20,7 @@ def per_kernel(path, counter, skip=5):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        k = r["Kernel_Name"].split("(")[0].replace("kmcd::", "")
+        k = re.sub(r"^void (k_\w+)<\d+>$", r"\1", r["Kernel_Name"].split("(")[0].replace("kmcd::", ""))
         acc[k].append(float(r["Counter_Value"]))
     return {k: (v[skip:] if len(v) > skip else v) for k, v in acc.items()}
 

@@ -1,5 +1,6 @@
 """Summarise a rocprofv3 kernel-trace CSV: per-kernel mean duration (µs),
 skipping the first `skip` launches of each kernel (clock ramp / warm-up)."""
+import re
 import csv
 import collections
 import sys
@@ -9,7 +10,7 @@ skip = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 rows = list(csv.DictReader(open(path)))
 by = collections.defaultdict(list)
 for r in rows:
-    name = r["Kernel_Name"].split("(")[0].replace("kmcd::", "")
+    name = re.sub(r"^void (k_\w+)<\d+>$", r"\1", r["Kernel_Name"].split("(")[0].replace("kmcd::", ""))
     by[name].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0)
 tot = 0
 out = []
