@@ -1143,13 +1143,6 @@ int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out) {
                 c[0], c[1], c[2], c[3], c[4], c[5], r[0], r[1], r[2], r[3]);
       }
       const uint64_t* t = s->ctl_host->stamps;
-#ifdef WALK_STATS
-      fprintf(stderr, "kmc walk AA %llu %llu %llu AB %llu %llu %llu BA %llu %llu %llu BB %llu %llu %llu "
-              "(walked, within xy reach, passing; cumulative)\n",
-              (unsigned long long)t[0], (unsigned long long)t[4], (unsigned long long)t[8], (unsigned long long)t[1],
-              (unsigned long long)t[5], (unsigned long long)t[9], (unsigned long long)t[2], (unsigned long long)t[6],
-              (unsigned long long)t[10], (unsigned long long)t[3], (unsigned long long)t[7], (unsigned long long)t[11]);
-#endif
       if (t[16])
         fprintf(stderr, "kmc stamps heavy stage %llu align %llu writeback %llu records %llu (cycles summed over "
                 "waves) complexes %llu max-cycles %llu members %llu\n",

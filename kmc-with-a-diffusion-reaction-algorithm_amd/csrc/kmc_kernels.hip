@@ -3181,15 +3181,6 @@ __device__ __forceinline__ void pair_push(PairBuf& b, int2 v) {
   b.v3 = b.n == 3 ? x : b.v3;
   ++b.n;
 }
-// the same for the lanes where `on` holds, without a branch (selects only;
-// CHK_PRED A/B builds)
-__device__ __forceinline__ void pair_push_if(PairBuf& b, bool on, uint32_t x) {
-  b.v0 = (on & (b.n == 0)) ? x : b.v0;
-  b.v1 = (on & (b.n == 1)) ? x : b.v1;
-  b.v2 = (on & (b.n == 2)) ? x : b.v2;
-  b.v3 = (on & (b.n == 3)) ? x : b.v3;
-  b.n += on ? 1 : 0;
-}
 // active lanes of a wave; entries mapped through f on the way out
 template <class F>
 __device__ __forceinline__ void pair_flush(const PairBuf& b, WgList& L, const SList& out, uint32_t* err, F f) {
@@ -3231,9 +3222,6 @@ __device__ __forceinline__ void pair_flush(const PairBuf& b, WgList& L, const SL
 #define REACH_CSITE 37.5f
 #ifndef CIS_SITE  // (A/B builds: 0 = the cis search around the record point, REACH_CIS)
 #define CIS_SITE 1
-#endif
-#ifndef CHK_PRED
-#define CHK_PRED 0
 #endif
 
 // ---------------------------------------------------------------- 4a. scan
@@ -3727,97 +3715,70 @@ __device__ __forceinline__ bool pair_scan_block(const KParams& P, const Dev& d, 
   Bc.n = 0;
   Br.n = 0;
   bool bad = false;  // a collision candidate whose record has no owner key
-  tile_walk(
-      G, T, T.u.l.wbits,
-      [&](int l, int seg, int hx, int* r0, int* r1) {
-        const int2 me = T.id[l];
-        bool prop = me.x < 0;  // proposal record: collision candidates
-        if (prop && me.y < 0) {
-          atomicOr(&d.ctl->err, ERR_RESOLVE);
-          prop = false;
-        }
-        const bool rx = rxn_item(me);
-        if (!prop && !rx) return false;
-        const bool mA = !(me.x & RID_LIG);
-        const float4 mp = T.pos[l];
-        // kind 0: the collision reach around the record, and for the cis
-        // search a square around its [3][3] site (any cis partner has its
-        // site within 16 Å of this one, its record within 20.3 Å of its site)
-        const float rc0 = prop ? (mA ? REACH_AA : REACH_AB) : 0.0f;
-        float x0lo = mp.x - rc0, x0hi = mp.x + rc0, y0lo = mp.y - rc0, y0hi = mp.y + rc0;
-        const bool cis = rx && !(me.x & RID_ST3);
-        if (cis) {
+  auto rng = [&](int l, int seg, int hx, int* r0, int* r1) {
+    const int2 me = T.id[l];
+    bool prop = me.x < 0;  // proposal record: collision candidates
+    if (prop && me.y < 0) {
+      atomicOr(&d.ctl->err, ERR_RESOLVE);
+      prop = false;
+    }
+    const bool rx = rxn_item(me);
+    if (!prop && !rx) return false;
+    const bool mA = !(me.x & RID_LIG);
+    const float4 mp = T.pos[l];
+    // kind 0: the collision reach around the record, and for the cis
+    // search a square around its [3][3] site (any cis partner has its
+    // site within 16 Å of this one, its record within 20.3 Å of its site)
+    const float rc0 = prop ? (mA ? REACH_AA : REACH_AB) : 0.0f;
+    float x0lo = mp.x - rc0, x0hi = mp.x + rc0, y0lo = mp.y - rc0, y0hi = mp.y + rc0;
+    const bool cis = rx && !(me.x & RID_ST3);
+    if (cis) {
 #if CIS_SITE
-          const float2 ms = site[l];
-          const float sxl = ms.x - REACH_CSITE, sxh = ms.x + REACH_CSITE, syl = ms.y - REACH_CSITE,
-                      syh = ms.y + REACH_CSITE;
+      const float2 ms = site[l];
+      const float sxl = ms.x - REACH_CSITE, sxh = ms.x + REACH_CSITE, syl = ms.y - REACH_CSITE,
+                  syh = ms.y + REACH_CSITE;
 #else
-          const float sxl = mp.x - REACH_CIS, sxh = mp.x + REACH_CIS, syl = mp.y - REACH_CIS,
-                      syh = mp.y + REACH_CIS;
+      const float sxl = mp.x - REACH_CIS, sxh = mp.x + REACH_CIS, syl = mp.y - REACH_CIS,
+                  syh = mp.y + REACH_CIS;
 #endif
-          x0lo = rc0 > 0.0f ? fminf(x0lo, sxl) : sxl;
-          x0hi = rc0 > 0.0f ? fmaxf(x0hi, sxh) : sxh;
-          y0lo = rc0 > 0.0f ? fminf(y0lo, syl) : syl;
-          y0hi = rc0 > 0.0f ? fmaxf(y0hi, syh) : syh;
-        }
-        float reach1 = prop ? (mA ? REACH_AB : REACH_BB) : 0.0f;
-        if (rx && !(me.x & RID_ST2) && NB > 0) reach1 = fmaxf(reach1, REACH_RL);
-        item_ranges(P, T, G, seg, hx, x0lo, x0hi, y0lo, y0hi, 0, r0, r1);
-        item_ranges(P, T, G, seg, hx, mp.x - reach1, mp.x + reach1, mp.y - reach1, mp.y + reach1, 1, r0 + 3,
-                    r1 + 3);
-        if (rc0 == 0.0f && !cis)
-          for (int k = 0; k < 3; ++k) r1[k] = r0[k];
-        if (reach1 == 0.0f)
-          for (int k = 3; k < 6; ++k) r1[k] = r0[k];
-        return true;
-      },
+      x0lo = rc0 > 0.0f ? fminf(x0lo, sxl) : sxl;
+      x0hi = rc0 > 0.0f ? fmaxf(x0hi, sxh) : sxh;
+      y0lo = rc0 > 0.0f ? fminf(y0lo, syl) : syl;
+      y0hi = rc0 > 0.0f ? fmaxf(y0hi, syh) : syh;
+    }
+    float reach1 = prop ? (mA ? REACH_AB : REACH_BB) : 0.0f;
+    if (rx && !(me.x & RID_ST2) && NB > 0) reach1 = fmaxf(reach1, REACH_RL);
+    item_ranges(P, T, G, seg, hx, x0lo, x0hi, y0lo, y0hi, 0, r0, r1);
+    item_ranges(P, T, G, seg, hx, mp.x - reach1, mp.x + reach1, mp.y - reach1, mp.y + reach1, 1, r0 + 3,
+                r1 + 3);
+    if (rc0 == 0.0f && !cis)
+      for (int k = 0; k < 3; ++k) r1[k] = r0[k];
+    if (reach1 == 0.0f)
+      for (int k = 3; k < 6; ++k) r1[k] = r0[k];
+    return true;
+  };
+  // one pair: pushed to the registers' buffers, then to the workgroup's lists
+  auto push = [&](bool colp, bool rxp, int il, int nl, int2 id) {
+    // (branches: most chunks have no passing pair, and the wave skips the
+    // pushes; measured faster than selects on every pair)
+    if (colp) {
+      if (id.y < 0) bad = true;
+      else if (Bc.n < 4) pair_push(Bc, make_int2(il, nl));
+      else col_emit(d, Lc, tile_global(T, il), tile_global(T, nl));
+    }
+    if (rxp) {
+      if (Br.n < 4) pair_push(Br, make_int2(il, nl));
+      else rxn_emit(d, Lr, tile_global(T, il), tile_global(T, nl));
+    }
+  };
+  tile_walk(
+      G, T, T.u.l.wbits, rng,
       [&](int il, int nl) {
         const int2 me = T.id[il], id = T.id[nl];
         const float4 mp = T.pos[il], rp = T.pos[nl];
-#if CHK_PRED  // (A/B builds: predicates without branches, pushes by selects)
-        const bool colp = (me.x < 0) & (me.y >= 0) & col_pair(me, mp, id, rp);
-        const bool rxp = rxn_item(me) & rxn_pair(me, mp, site[il], id, rp, site[nl]);
-#else
         const bool colp = me.x < 0 && me.y >= 0 && col_pair(me, mp, id, rp);
         const bool rxp = rxn_item(me) && rxn_pair(me, mp, site[il], id, rp, site[nl]);
-#endif
-#ifdef WALK_STATS  // diagnostic build: pairs walked / within the kind pair's xy reach / passing, by kind pair
-        {
-          const int c = ((me.x & RID_LIG) ? 2 : 0) + ((id.x & RID_LIG) ? 1 : 0);
-          const float dx = rp.x - mp.x, dy = rp.y - mp.y, R = c == 0 ? 58.0f : (c == 3 ? 131.5f : 106.0f);
-          const bool xy = dx * dx + dy * dy < R * R;
-          for (int k = 0; k < 4; ++k) {
-            const uint32_t w = __popcll(__ballot(c == k)), x = __popcll(__ballot(c == k && xy)),
-                           v = __popcll(__ballot(c == k && (colp || rxp)));
-            if (__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) {
-              atomicAdd((unsigned long long*)&d.ctl->stamps[k], (unsigned long long)w);
-              atomicAdd((unsigned long long*)&d.ctl->stamps[4 + k], (unsigned long long)x);
-              atomicAdd((unsigned long long*)&d.ctl->stamps[8 + k], (unsigned long long)v);
-            }
-          }
-        }
-#endif
-#if CHK_PRED
-        bad |= colp & (id.y < 0);
-        const bool cp = colp & (id.y >= 0);
-        const uint32_t x = (uint32_t)il | (uint32_t)nl << 16;
-        if (cp & (Bc.n >= 4)) col_emit(d, Lc, tile_global(T, il), tile_global(T, nl));
-        pair_push_if(Bc, cp & (Bc.n < 4), x);
-        if (rxp & (Br.n >= 4)) rxn_emit(d, Lr, tile_global(T, il), tile_global(T, nl));
-        pair_push_if(Br, rxp & (Br.n < 4), x);
-#else
-        // (branches: most chunks have no passing pair, and the wave skips the
-        // pushes; measured faster than selects on every pair)
-        if (colp) {
-          if (id.y < 0) bad = true;
-          else if (Bc.n < 4) pair_push(Bc, make_int2(il, nl));
-          else col_emit(d, Lc, tile_global(T, il), tile_global(T, nl));
-        }
-        if (rxp) {
-          if (Br.n < 4) pair_push(Br, make_int2(il, nl));
-          else rxn_emit(d, Lr, tile_global(T, il), tile_global(T, nl));
-        }
-#endif
+        push(colp, rxp, il, nl, id);
       });
   if (bad) atomicOr(&d.ctl->err, ERR_RESOLVE);
   S(d, 5);
