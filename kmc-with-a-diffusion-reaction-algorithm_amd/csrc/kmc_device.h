@@ -116,6 +116,9 @@ enum : uint32_t { S_ACC = 1, S_PEND = 2, S_REJ = 3 };  // unit fate this step (a
 #ifndef BEAD_BLOCK
 #define BEAD_BLOCK 1
 #endif
+#ifndef BEAD_BS  // slots per block (a power of two dividing 64; A/B builds: smaller blocks put a protein's rows
+#define BEAD_BS 64  // fewer cache lines apart for the gathers, the streams' rows fewer bytes long)
+#endif
 #ifndef ROW_PERM  // (A/B builds) blocked layout: the rows the gathers read first in each block
 #define ROW_PERM 0
 #endif
@@ -135,7 +138,7 @@ __host__ __device__ __forceinline__ int bead_row(int r, int rows) {
 __host__ __device__ __forceinline__ size_t bead_elem(int i, int r, int n, int rows) {
 #if BEAD_BLOCK
   (void)n;
-  return ((size_t)(i >> 6) * rows + bead_row(r, rows)) * 64 + (i & 63);
+  return ((size_t)(i / BEAD_BS) * rows + bead_row(r, rows)) * BEAD_BS + (i % BEAD_BS);
 #else
   (void)rows;
   return (size_t)r * n + i;

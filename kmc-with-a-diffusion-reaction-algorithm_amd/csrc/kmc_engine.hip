@@ -913,6 +913,8 @@ static int launch_step(kmc_sim* s, bool re_sort) {
   // exact tests of the candidates
   TIMED(KI_COL_EXACT, {
 #if DENSE_KERNEL
+    // (a second stream for it, forked after the pair scan and joined before
+    // the rounds, cost 15 us per step at C3 for the 5 us launch it hides)
     k_col_dense<<<64, T, 0, st>>>(K, d);
     if (s->debug_sync && hipStreamSynchronize(st) != hipSuccess)
       return fail(s, KMC_ERR_HIP, "KMC_DEBUG_SYNC: k_col_dense failed in step " + std::to_string(s->launch_base));
