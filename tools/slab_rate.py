@@ -1,0 +1,51 @@
+"""Step rate of one trajectory split into G slabs (slabs.py) against the
+single-handle engine on the same GPU, from the same placement (diagnostic
+measurement, not the bench: the slab driver exchanges halos through the host
+every step).
+  python -u tools/slab_rate.py [workload] [G ...] [--steps K]
+Prints per G: ms/step, the driver's counters (units exchanged / verified per
+step, re-partitions, rollbacks) and the single-handle ms/step.
+"""
+import argparse
+import importlib
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+PKG = "kmc-with-a-diffusion-reaction-algorithm_amd"
+engine = importlib.import_module(PKG + ".engine")
+slabs = importlib.import_module(PKG + ".slabs")
+workloads = importlib.import_module(PKG + ".workloads")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("workload", nargs="?", default="C2")
+    ap.add_argument("G", nargs="*", type=int, default=[2, 4])
+    ap.add_argument("--steps", type=int, default=100)
+    a = ap.parse_args()
+    p = workloads.params(a.workload, seed=1)
+    st = engine.host_init_random(p)
+    with engine.Simulation(p) as sim:
+        sim.set_state(st)
+        sim.step(10)
+        t = time.time()
+        sim.step(a.steps)
+        one = (time.time() - t) / a.steps * 1e3
+    print(f"{a.workload} single handle: {one:.3f} ms/step", flush=True)
+    for G in a.G:
+        t0 = time.time()
+        recs, ranks = slabs.run_local(p, st, G, a.steps, lambda q: engine.Simulation(q), gather_every=a.steps)
+        ms = (time.time() - t0) / a.steps * 1e3
+        s = ranks[0].stats
+        print(f"{a.workload} G={G}: {ms:.3f} ms/step (incl. start), exchanged {s['exchanged'] / a.steps:.0f} "
+              f"verified {s['verified'] / a.steps:.0f} units/step, rebuilds {s['rebuilds']}, rollbacks "
+              f"{s['rollbacks']}, held {s['held']} of {p.n_a + p.n_b}", flush=True)
+        for r in ranks:
+            r.close()
+
+
+if __name__ == "__main__":
+    main()
