@@ -336,7 +336,9 @@ __device__ __forceinline__ void mark_bond_change(const KParams& P, const Dev& d,
 // lowest-indexed ligand of its component; the BFS of any other ligand of the
 // component finds a lower one among its members and registers nothing.
 #define BFS_QCAP 32
+#ifndef BFS_BATCH  // queued nodes whose links are loaded together (A/B builds)
 #define BFS_BATCH 4
+#endif
 
 // the neighbours in three fixed slots (-1 = none), in BFS order
 __device__ __forceinline__ void nbrs3(const KParams& P, const Dev& d, int x, int* y) {
@@ -2170,6 +2172,9 @@ __device__ __forceinline__ void move_member(const KParams& P, const Dev& d, int 
   if (!ext) atomicOr(&d.cx_ext[root - P.NA], 1u);
 }
 
+#ifndef CXCHECK_BATCH  // (A/B builds: 0 = one chain of loads per bond site)
+#define CXCHECK_BATCH 1
+#endif
 __global__ void __launch_bounds__(256) k_cx_check(KParams P, Dev d) {
   const int NA = P.NA, NB = P.NB;
   const uint32_t n = d.ctl->n_cx;
@@ -2182,8 +2187,32 @@ __global__ void __launch_bounds__(256) k_cx_check(KParams P, Dev d) {
     const uint32_t xb = d.cx_ext[desc.x & CXD_LB];  // (set by k_move_members, cleared here)
     if (xb) d.cx_ext[desc.x & CXD_LB] = 0u;
     bool heavy = nB != 1;
+#if CXCHECK_BATCH
     if (!heavy) {
+      // lay-down and every bond's alignment tests (pure: evaluated for all
+      // three sites at once, whatever the others gave), in three rounds of
+      // loads instead of one chain per site: the links, then the partners and
+      // the bond beads, then the cis beads (clamped indices: a site without a
+      // bond reads slot 0 and discards it)
       const int lb = desc.x;  // the root: the complex's only ligand
+      int a1r[3], a2r[3];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) a1r[j] = B_NEI(d, lb, j + 2);
+      heavy = N.B(lb, 1, 2, 2) != (N.B(lb, 1, 1, 2) + P.rb);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) a2r[j] = A_NEI3(d, a1r[j] > 0 ? a1r[j] - 1 : 0);
+      bool mis[3];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) mis[j] = bond_misaligned(P, N, lb, j + 2, a1r[j] > 0 ? a1r[j] - 1 : 0);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const bool cm = cis_misaligned(P, N, a1r[j] > 0 ? a1r[j] - 1 : 0, a2r[j] > 0 ? a2r[j] - 1 : 0);
+        heavy |= a1r[j] > 0 && (mis[j] || (a2r[j] != 0 && cm));
+      }
+    }
+#else
+    if (!heavy) {
+      const int lb = desc.x;
       heavy = N.B(lb, 1, 2, 2) != (N.B(lb, 1, 1, 2) + P.rb);
 #pragma unroll
       for (int j = 2; j <= 4; ++j) {
@@ -2193,6 +2222,7 @@ __global__ void __launch_bounds__(256) k_cx_check(KParams P, Dev d) {
         heavy |= bond_misaligned(P, N, lb, j, a1) || (a2ref != 0 && cis_misaligned(P, N, a1, a2ref - 1));
       }
     }
+#endif
     if (heavy) {
       d.cx_heavy[atomicAdd(&d.ctl->n_heavy, 1u)] = make_int4(desc.x | CXD_MOVED, desc.y, desc.z, desc.w);
       continue;
@@ -3453,12 +3483,14 @@ void dense_block(const KParams& P, const Dev& d, int4 blk, uint32_t tag) {
   });
 }
 
-// The dense tiles in a kernel of their own (DENSE_KERNEL): the brute force's
-// registers would otherwise set k_col_exact's occupancy (107 against 58
-// VGPRs); it exits at once when no tile overflowed (every step at the
-// benchmark densities).
+// The dense tiles: in k_col_exact's first workgroups (DENSE_KERNEL 0), or in
+// a kernel of their own.  The own kernel kept k_col_exact at 58 VGPRs against
+// the brute force's 107 (round 2); since the record refinement k_col_exact
+// holds ~100 anyway, and the separate launch (4.8 µs, empty at the benchmark
+// densities) is the larger cost: C3 34.1 -> 30.1 µs for the pair, C5 equal
+// (profiles/r05/tail/r6a_*).
 #ifndef DENSE_KERNEL
-#define DENSE_KERNEL 1
+#define DENSE_KERNEL 0
 #endif
 __global__ void k_col_dense(KParams P, Dev d) {
   const uint32_t tag = (d.ctl->step & 0x3fffffffu) << 2;
@@ -3913,9 +3945,27 @@ __device__ __forceinline__ void rxn_exact(const KParams& P, const Dev& d, uint32
 // position where it is (R of a rejected unit, which the revert copies into
 // R_new), so neither half waits for the other; both are done before k_match
 // snaps associated receptors in R_new.
+#ifndef COMMIT_MIX  // (A/B builds: 0 = the revert's workgroups first)
+#define COMMIT_MIX 1
+#endif
 __global__ void k_commit_rxn(KParams P, Dev d, int nrej) {
-  if ((int)blockIdx.x < nrej) rej_commit(P, d, blockIdx.x, (uint32_t)nrej);
-  else rxn_exact(P, d, blockIdx.x - (uint32_t)nrej, gridDim.x - (uint32_t)nrej);
+  const uint32_t b = blockIdx.x, nr = (uint32_t)nrej, nx = gridDim.x - nr;
+#if COMMIT_MIX
+  // the two halves' workgroups alternate while both have some left, so both
+  // are resident from the start (the dispatcher goes in workgroup order)
+  const uint32_t m = min(nr, nx);
+  if (b < 2 * m) {
+    if (b & 1) rxn_exact(P, d, b >> 1, nx);
+    else rej_commit(P, d, b >> 1, nr);
+  } else if (nr > nx) {
+    rej_commit(P, d, b - m, nr);
+  } else {
+    rxn_exact(P, d, b - m, nx);
+  }
+#else
+  if (b < nr) rej_commit(P, d, b, nr);
+  else rxn_exact(P, d, b - nr, nx);
+#endif
 }
 
 // ---------------------------------------------------------------- greedy
