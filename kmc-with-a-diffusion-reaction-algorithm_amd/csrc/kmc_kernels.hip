@@ -3661,9 +3661,6 @@ __device__ __forceinline__ void rej_copy(const KParams& P, const Dev& d, int m, 
 // of k_match, which move receptors in R_new that a revert must restore first — DESIGN.md §8)
 #error "REJ_SIDE is wrong by design"
 #endif
-#ifndef REJ_SPEC  // (A/B builds: 0 = a complex's row / a dimer's partner read after the kind)
-#define REJ_SPEC 1
-#endif
 #ifndef REJ_UNROLL  // rejected units whose lookups a lane group has in flight at once
 #define REJ_UNROLL 1
 #endif
@@ -3689,21 +3686,6 @@ __device__ __forceinline__ void rej_commit(const KParams& P, const Dev& d, uint3
 #pragma unroll
     for (int u = 0; u < U; ++u)
       if (sl[u] >= 0) sl[u] = d.slot_of[sl[u]];
-#if REJ_SPEC
-    // the unit kind and what each kind needs next (a complex's row, a dimer's
-    // partner) in one round: the latter read at clamped indices whatever the
-    // kind, and the kind picks
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int s = sl[u], NB = P.NB;
-      const int b = min(max(s - NA, 0), max(NB - 1, 0)), a = min(max(s, 0), max(NA - 1, 0));
-      kind[u] = s >= 0 ? d.ukind[s] : (uint8_t)U_NONE;
-      const int co = NB > 0 ? d.cx_off[b] : 0, cs = NB > 0 ? d.cx_size[b] : 0, qa = NA > 0 ? A_NEI3(d, a) : 0;
-      off[u] = kind[u] == U_COMPLEX ? co : 0;
-      nm[u] = kind[u] == U_COMPLEX ? cs : (kind[u] == U_DIMER ? 2 : (s >= 0 ? 1 : 0));
-      q[u] = kind[u] == U_DIMER ? qa - 1 : -1;
-    }
-#else
 #pragma unroll
     for (int u = 0; u < U; ++u) kind[u] = sl[u] >= 0 ? d.ukind[sl[u]] : (uint8_t)U_NONE;
 #pragma unroll
@@ -3719,7 +3701,6 @@ __device__ __forceinline__ void rej_commit(const KParams& P, const Dev& d, uint3
         q[u] = A_NEI3(d, sl[u]) - 1;
       }
     }
-#endif
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       auto member = [&](int k) { return kind[u] == U_COMPLEX ? d.members[off[u] + k] : (k ? q[u] : sl[u]); };
@@ -3893,9 +3874,6 @@ __global__ void __launch_bounds__(PAIR_THREADS, PAIR_WAVES) k_pair_scan(KParams 
 // and cis gates (1954-1985 / 2009-2039) on each pair; a pair becomes an
 // accepting edge when its keyed draw is below the acceptance probability.
 // The greedy kernels below replay the reference's loop order on the edges.
-#ifndef RXN_BATCH  // (A/B builds: 0 = each site's status and beads loaded in turn)
-#define RXN_BATCH 1
-#endif
 // (workgroup blk of nblk taking part)
 __device__ __forceinline__ void rxn_exact(const KParams& P, const Dev& d, uint32_t blk, uint32_t nblk) {
   const int NA = P.NA, NB = P.NB;
@@ -3916,36 +3894,11 @@ __device__ __forceinline__ void rxn_exact(const KParams& P, const Dev& d, uint32
     const Beads& NQ = rb.x < 0 ? d.nxt : d.cur;
     if (q >= NA) {
       int lb = q - NA;
-#if RXN_BATCH
-      // the three sites' status words and distance-gate beads in one round
-      // of loads (the loop below would chain them site by site: its atomics
-      // keep the compiler from hoisting them)
-      bool gate[3];
-      {
-        int st[3];
-        double bx[3], by[3], bz[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          st[k] = B_ST(d, lb, k + 2);
-          bx[k] = NQ.B(lb, k + 2, 2, 0);
-          by[k] = NQ.B(lb, k + 2, 2, 1);
-          bz[k] = NQ.B(lb, k + 2, 2, 2);
-        }
-        const double ax = NI.A(i, 3, 2, 0), ay = NI.A(i, 3, 2, 1), az = NI.A(i, 3, 2, 2);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) gate[k] = st[k] == 0 && d2(bx[k] - ax, by[k] - ay, bz[k] - az) < P.T_bond;
-      }
-      if (!(gate[0] || gate[1] || gate[2])) continue;
-#endif
       for (int k = 2; k <= 4; ++k) {
-#if RXN_BATCH
-        if (!gate[k - 2]) continue;
-#else
         if (B_ST(d, lb, k) != 0) continue;
         double ddx = NQ.B(lb, k, 2, 0) - NI.A(i, 3, 2, 0), ddy = NQ.B(lb, k, 2, 1) - NI.A(i, 3, 2, 1),
                ddz = NQ.B(lb, k, 2, 2) - NI.A(i, 3, 2, 2);
         if (!(d2(ddx, ddy, ddz) < P.T_bond)) continue;
-#endif
         if (P.dbg_cand) atomicAdd(&d.ctl->rxn_kind[2], 1u);
         double ot = gettheta(NI.A(i, 3, 1, 0) - NI.A(i, 3, 2, 0), NI.A(i, 3, 1, 1) - NI.A(i, 3, 2, 1),
                              NI.A(i, 3, 1, 2) - NI.A(i, 3, 2, 2), NQ.B(lb, k, 1, 0) - NQ.B(lb, k, 2, 0),
