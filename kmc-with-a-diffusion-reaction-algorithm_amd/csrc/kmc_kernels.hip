@@ -2644,8 +2644,8 @@ __device__ __forceinline__ void wg_flush2(WgList& L0, const SList& o0, WgList& L
 #define NSEG_MAX (NPART * HALO_MAX)
 #define HOME_MAX (TILE_MAX + 4)
 #define HSEG_MAX (2 * HOME_MAX)
-#ifndef SUBC  // sub-columns per cell in the LDS bins (x extent of the cut stencils: 130 / SUBC Å steps)
-#define SUBC 2
+#ifndef SUBC  // sub-columns per cell in the LDS bins (x extent of the cut stencils: 130 / SUBC Å steps;
+#define SUBC 3  // A/B, profiles/r05/ab_walk/r6i_*: 2 -> 3, k_pair_scan 114.1 -> 111.5 us at C3, 1265 -> 1228 at C5)
 #endif
 #define CFLAT_MAX (NSEG_MAX * (HALO_MAX * SUBC + 1) + 1)
 #define SCAN_PER ((CFLAT_MAX + 255) / 256)  // bin counters per thread in the block scans
@@ -2741,12 +2741,26 @@ __device__ __forceinline__ void scan_ld(const int* a, int t, int m, int* v) {
     v[3] = x.w;
     return;
   }
+  if (SCAN_PER % 2 == 0 && SCAN_PER * t + SCAN_PER - 1 < m) {  // 8-byte accesses
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; k += 2) {
+      const int2 x = *reinterpret_cast<const int2*>(a + SCAN_PER * t + k);
+      v[k] = x.x;
+      v[k + 1] = x.y;
+    }
+    return;
+  }
 #pragma unroll
   for (int k = 0; k < SCAN_PER; ++k) v[k] = SCAN_PER * t + k < m ? a[SCAN_PER * t + k] : 0;
 }
 __device__ __forceinline__ void scan_st(int* a, int t, int m, const int* v) {
   if (SCAN_PER == 4 && 4 * t + 3 < m) {
     *reinterpret_cast<int4*>(a + 4 * t) = make_int4(v[0], v[1], v[2], v[3]);
+    return;
+  }
+  if (SCAN_PER % 2 == 0 && SCAN_PER * t + SCAN_PER - 1 < m) {
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; k += 2) *reinterpret_cast<int2*>(a + SCAN_PER * t + k) = make_int2(v[k], v[k + 1]);
     return;
   }
 #pragma unroll
