@@ -236,6 +236,19 @@ extern "C" {
 
 const char* kmc_last_error(const kmc_sim* s) { return s ? s->err.c_str() : "null handle"; }
 
+// Tile side of the LDS scans for rho proteins per cell: about 200 proposal
+// records per 256-thread workgroup, halo records well inside TCAP (a tile
+// whose records still overflow goes onto the dense list and is brute-forced
+// from global memory: the mean is kept at 0.75 TCAP, > 7 Poisson sigmas below
+// TCAP at the benchmark densities).  KMC_TILE overrides (tests, sweeps).
+static int choose_tile(double rho) {
+  int t = TILE_MAX;
+  while (t > 4 && (t * t * rho > 205.0 || (t + 2) * (t + 2) * 2.0 * rho > 0.75 * TCAP)) --t;
+  const char* te = getenv("KMC_TILE");
+  if (te && *te) t = std::max(2, std::min(TILE_MAX, atoi(te)));
+  return t;
+}
+
 int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   if (!p || !out) return KMC_ERR_ARG;
   *out = nullptr;
@@ -407,18 +420,9 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   const char* oc = getenv("KMC_DEBUG_TOUT_CAP");
   K.tout_cap = TOUT_CAP;
   if (oc && *oc) K.tout_cap = std::max(0, std::min(TOUT_CAP, atoi(oc)));
-  // tile side of the LDS scans: about 200 proposal records per 256-thread
-  // workgroup, halo records well inside TCAP (mean density of the box)
+  // tile side of the LDS scans (mean density of the box)
   {
-    const double rho = (double)N * K.cs * K.cs / std::max(1.0, p->box_x * p->box_y);  // proteins per cell
-    int t = TILE_MAX;
-    // (a tile whose records still overflow TCAP goes onto the dense list and
-    // is brute-forced from global memory by k_col_dense: the mean is kept at
-    // 0.75 TCAP, > 7 Poisson sigmas below TCAP at the benchmark densities)
-    while (t > 4 && (t * t * rho > 205.0 || (t + 2) * (t + 2) * 2.0 * rho > 0.75 * TCAP)) --t;
-    const char* te = getenv("KMC_TILE");
-    if (te && *te) t = std::max(2, std::min(TILE_MAX, atoi(te)));
-    K.tile = t;
+    K.tile = choose_tile((double)N * K.cs * K.cs / std::max(1.0, p->box_x * p->box_y));
     const char* fb = getenv("KMC_FULL_BFS");
     s->always_full = fb && *fb == '1';
     const char* ds = getenv("KMC_DEBUG_SCAN_STAGE");
@@ -1428,6 +1432,30 @@ int kmc_dd_set_state(kmc_sim* s, const kmc_state_view* v, const int32_t* gid, co
   HIPCHK(s, hipMemcpy(s->dd_gid, gid, sizeof(int32_t) * N, hipMemcpyHostToDevice));
   HIPCHK(s, hipMemcpy(s->dd_own, own, (size_t)N, hipMemcpyHostToDevice));
   HIPCHK(s, hipMemcpy(s->dd_x0, x0.data(), sizeof(double) * N, hipMemcpyHostToDevice));
+  // a window holds its slab's units in part of the box's x range: its tiles
+  // are sized from the density where the proteins are (the share of 1024 x
+  // buckets holding any), not from the box's mean — at twice the mean density
+  // every occupied tile would overflow the LDS staging into the dense path
+  {
+    std::vector<uint8_t> occ(1024, 0);
+    const double L = s->p.box_x;
+    for (int i = 0; i < N; ++i) {
+      const double u = x0[i] - L * std::floor(x0[i] / L);
+      occ[std::min(1023, std::max(0, (int)(u / L * 1024.0)))] = 1;
+    }
+    int n_occ = 0;
+    for (uint8_t o : occ) n_occ += o;
+    const double f = std::max(1, n_occ) / 1024.0;
+    const int t = choose_tile((double)N * s->K.cs * s->K.cs / std::max(1.0, f * L * s->p.box_y));
+    if (t != s->K.tile) {
+      s->K.tile = t;
+      dfree(s, s->d.tout);
+      dfree(s, s->d.tout_n);
+      s->ntiles = ((s->K.ncx + t - 1) / t) * ((s->K.ncy + t - 1) / t);
+      if (dalloc(s, &s->d.tout, (size_t)s->ntiles * TOUT_CAP) != KMC_OK || dalloc(s, &s->d.tout_n, (size_t)s->ntiles) != KMC_OK)
+        return fail(s, KMC_ERR_HIP, "dd: tile buffers");
+    }
+  }
   s->K.dd = 1;
   s->d.gid = s->dd_gid;
   s->d.dd_own = s->dd_own;
