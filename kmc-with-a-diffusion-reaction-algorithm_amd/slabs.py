@@ -51,6 +51,7 @@ from __future__ import annotations
 
 import os
 import threading
+import time
 from dataclasses import dataclass, field
 from typing import Callable, List, Optional
 
@@ -315,7 +316,8 @@ class SlabRank:
         self.history: list = []  # global records since the checkpoint (replay check)
         self.stats = dict(steps=0, rebuilds=0, rebuild_bond=0, rebuild_jumpers=0, rollbacks=0, replayed=0, xcol=0,
                           xbond=0,
-                          exchanged=0, verified=0, jumpers=0, held=0, owned=0, why=[])
+                          exchanged=0, verified=0, jumpers=0, held=0, owned=0, why=[],
+                          sec=dict(step=0.0, export=0.0, comm=0.0, imp=0.0, jumpers=0.0, gather=0.0, rebuild=0.0))
         self.last_global: Optional[capi.HostState] = None
         self._xc = (0, 0)
         self._njump = 0  # jumpers after the last step, all slabs
@@ -340,6 +342,11 @@ class SlabRank:
         self._rebuild_from(hs)
 
     def _rebuild_from(self, hs: capi.HostState) -> None:
+        t0 = time.perf_counter()
+        self._rebuild_inner(hs)
+        self.stats["sec"]["rebuild"] += time.perf_counter() - t0
+
+    def _rebuild_inner(self, hs: capi.HostState) -> None:
         self.ckpt = hs.copy()
         self.ckpt.counters[:] = self.counters
         self.ckpt.step = self.step_no
@@ -454,8 +461,12 @@ class SlabRank:
 
     def _step_exchange(self) -> Optional[np.ndarray]:
         w = self.win
+        sec = self.stats["sec"]  # host seconds by phase (tools/slab_rate.py)
+        t0 = time.perf_counter()
         part = self.eng.step(1)[0]
         xcol, xbond = self.eng.dd_counters()
+        t1 = time.perf_counter()
+        sec["step"] += t1 - t0
         dcol, dbond = xcol - self._xc[0], xbond - self._xc[1]
         self._xc = (xcol, xbond)
         # halo exchange: my owned proteins' end state to every window holding them
@@ -467,7 +478,11 @@ class SlabRank:
                 continue
             beads, ints = self.eng.dd_export(ids)
             out.append((w.gids[ids], beads, self._links(ints, ids, True, w)))
+        t2 = time.perf_counter()
+        sec["export"] += t2 - t1
         got = self.comm.alltoall(self.rank, out)
+        t3 = time.perf_counter()
+        sec["comm"] += t3 - t2
         bad = 0
         nver = 0
         for src, msg in enumerate(got):
@@ -506,9 +521,14 @@ class SlabRank:
             if rc != 0:
                 raise SlabError(f"rank {self.rank}: window state invalid ({rc}) after the import of step "
                                 f"{self.step_no + 1}: {_engine.load_library().kmc_host_last_error().decode()}")
+        t4 = time.perf_counter()
+        sec["imp"] += t4 - t3
         jbad = self._jumper_check()
+        t5 = time.perf_counter()
+        sec["jumpers"] += t5 - t4
         # the step's record from every slab's share; checks, triggers
         shares = self.comm.allgather(self.rank, (part.copy(), bad, jbad, dbond, dcol, self._my_jumpers))
+        sec["gather"] += time.perf_counter() - t5
         if any(s[1] or s[2] for s in shares):
             self.stats["why"].append((self.step_no + 1, "verify" if any(s[1] for s in shares) else "jumper",
                                       sum(s[1] for s in shares), sum(s[2] for s in shares)))

@@ -44,6 +44,9 @@ def main():
             recs, ranks = slabs.run_local(p, st, G, k, lambda q: engine.Simulation(q), gather_every=k)
             tt.append(time.time() - t0)
             s = ranks[0].stats
+            if k > 1:
+                print("  rank 0 host ms/step by phase: " + ", ".join(
+                    f"{n} {v / k * 1e3:.3f}" for n, v in s["sec"].items()), flush=True)
             for r in ranks:
                 r.close()
         ms = (tt[1] - tt[0]) / (a.steps - 1) * 1e3
