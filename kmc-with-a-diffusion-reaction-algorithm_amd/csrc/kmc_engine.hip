@@ -3,7 +3,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <hipcub/hipcub.hpp>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -73,14 +72,13 @@ struct kmc_sim {
   // slot order (kmc_kernels.hip §slot order): scratch of the re-sort
   int64_t resort_every = 100, since_resort = 0;
   int key_bits = 1;
-  uint64_t *skeys = nullptr, *skeys2 = nullptr;  // (cell << 32) | grouping key
+  uint64_t *skeys = nullptr, *skeys2 = nullptr;  // packed slot keys (k_slot_keys), radix sort ping-pong
   int group_sort = 2;  // 1: members of one unit in consecutive slots; 2: and complexes after the free units; 0: cell only
   int32_t *svals = nullptr, *svals2 = nullptr, *perm = nullptr, *newslot = nullptr;
   int32_t *a_tmp = nullptr, *b_tmp = nullptr, *id_tmp = nullptr;
-  void* sort_tmp = nullptr;
-  size_t sort_tmp_bytes = 0;
-  void* scan_tmp = nullptr;  // hipcub exclusive scan of the home cell counts (home_build)
-  size_t scan_tmp_bytes = 0;
+  int32_t* rs_cnt = nullptr;     // [256][tiles] digit counts of the radix sort -> first output positions
+  int32_t* rs_tot = nullptr;     // [256] digit totals of a radix pass
+  int32_t* scan_part = nullptr;  // tile sums of dev_scan
   int32_t* hcnt = nullptr;   // [ncell+1] home cell counts (home_build)
   // per-kernel timing: a ring of TRING steps of event pairs, read back lazily
   uint64_t tmask = 0;
@@ -384,6 +382,12 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   rc |= dalloc(s, &d.cx_list, (size_t)d.mcap / 2);  // kept across steps: every registration since the last rebuild
   rc |= dalloc(s, &d.cx_heavy, NB);
   rc |= dalloc(s, &s->hcnt, s->ncell + 1);
+  {
+    const size_t nblk = ((size_t)N + RS_TILE - 1) / RS_TILE;
+    rc |= dalloc(s, &s->rs_cnt, 256 * nblk);
+    rc |= dalloc(s, &s->rs_tot, 256);
+    rc |= dalloc(s, &s->scan_part, ((size_t)s->ncell + 1 + SCAN_TILE - 1) / SCAN_TILE);
+  }
   rc |= dalloc(s, &d.hstart, s->ncell + 1);
   rc |= dalloc(s, &d.home, N);
   rc |= dalloc(s, &d.rec, (size_t)2 * N);
@@ -449,33 +453,14 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
     const uint64_t kmax = (uint64_t)K.ncx * K.ncy;  // row-major cell keys (k_slot_keys)
     s->key_bits = 1;
     while ((1ull << s->key_bits) < kmax) ++s->key_bits;
+    if (s->key_bits + 33 > 64) {  // the packed slot key: unit (< 2^31), cell, complex flag, kind
+      kmc_destroy(s);
+      return KMC_ERR_ARG;
+    }
     const char* re = getenv("KMC_RESORT");
     if (re && *re) s->resort_every = atoll(re);
-    size_t tb = 0;
-    int nmax = std::max(NA, NB);
     const char* gs = getenv("KMC_GROUP_SORT");
     if (gs && *gs) s->group_sort = std::max(0, std::min(2, atoi(gs)));
-    if (hipcub::DeviceRadixSort::SortPairs(nullptr, tb, s->skeys, s->skeys2, s->svals, s->svals2, nmax, 0,
-                                           64, s->stream) != hipSuccess) {
-      kmc_destroy(s);
-      return KMC_ERR_HIP;
-    }
-    s->sort_tmp_bytes = std::max<size_t>(tb, 16);
-    if (dalloc(s, (uint8_t**)&s->sort_tmp, s->sort_tmp_bytes) != KMC_OK) {
-      kmc_destroy(s);
-      return KMC_ERR_HIP;
-    }
-    tb = 0;
-    if (hipcub::DeviceScan::ExclusiveSum(nullptr, tb, s->hcnt, s->d.hstart, s->ncell + 1, s->stream) !=
-        hipSuccess) {
-      kmc_destroy(s);
-      return KMC_ERR_HIP;
-    }
-    s->scan_tmp_bytes = std::max<size_t>(tb, 16);
-    if (dalloc(s, (uint8_t**)&s->scan_tmp, s->scan_tmp_bytes) != KMC_OK) {
-      kmc_destroy(s);
-      return KMC_ERR_HIP;
-    }
     // per-tile outlier buckets of the pair scan (counters zero between steps)
     s->ntiles = ((K.ncx + K.tile - 1) / K.tile) * ((K.ncy + K.tile - 1) / K.tile);
     if (dalloc(s, &s->d.tout, (size_t)s->ntiles * TOUT_CAP) != KMC_OK ||
@@ -536,6 +521,52 @@ __global__ void k_iota(int32_t* a, int32_t* b, int n) {
   if (i < n) a[i] = b[i] = i;
 }
 
+// Exclusive scan of n counts (in may be out): tile sums, their scan, the tiles.
+static void dev_scan(kmc_sim* s, const int32_t* in, int32_t* out, int n, hipStream_t st) {
+  const int nb = (n + SCAN_TILE - 1) / SCAN_TILE;
+  k_scan_part<<<nb, 256, 0, st>>>(in, n, s->scan_part);
+  k_scan_top<<<1, 256, 0, st>>>(s->scan_part, nb);
+  k_scan_down<<<nb, 256, 0, st>>>(in, out, n, s->scan_part);
+}
+
+// Stable LSD radix sort of the N packed slot keys (skeys, svals) over their
+// low nbits, 8 bits a pass; returns the buffer holding the sorted values.
+static int32_t* radix_sort(kmc_sim* s, int nbits, hipStream_t st, uint64_t** keys_out) {
+  const int N = s->K.N, nblk = (N + RS_TILE - 1) / RS_TILE;
+  uint64_t *ka = s->skeys, *kb = s->skeys2;
+  int32_t *va = s->svals, *vb = s->svals2;
+  if (nblk == 0) nbits = 0;  // (no slots: nothing to launch)
+  for (int shift = 0; shift < nbits; shift += 8) {
+    k_rs_hist<<<nblk, 256, 0, st>>>(ka, N, shift, s->rs_cnt, nblk);
+    k_rs_rows<<<256, 256, 0, st>>>(s->rs_cnt, nblk, s->rs_tot);
+    k_rs_scatter<<<nblk, 256, 0, st>>>(ka, va, kb, vb, N, shift, s->rs_cnt, s->rs_tot, nblk);
+    std::swap(ka, kb);
+    std::swap(va, vb);
+  }
+  *keys_out = ka;
+  return va;
+}
+
+// debug (KMC_DEBUG_SYNC=1): the sorted keys non-decreasing, equal keys in
+// their input order (stability), the values of each kind a permutation
+static int check_sort(kmc_sim* s, const uint64_t* dk, const int32_t* dv) {
+  const int N = s->K.N, NA = s->K.NA;
+  std::vector<uint64_t> k((size_t)N);
+  std::vector<int32_t> v((size_t)N);
+  HIPCHK(s, hipStreamSynchronize(s->stream));
+  HIPCHK(s, hipMemcpy(k.data(), dk, sizeof(uint64_t) * N, hipMemcpyDeviceToHost));
+  HIPCHK(s, hipMemcpy(v.data(), dv, sizeof(int32_t) * N, hipMemcpyDeviceToHost));
+  std::vector<uint8_t> seen((size_t)N, 0);
+  for (int i = 0; i < N; ++i) {
+    const int kind = i >= NA, base = kind ? NA : 0, nk = kind ? N - NA : NA;
+    if (v[i] < 0 || v[i] >= nk || seen[(size_t)base + v[i]]++)
+      return fail(s, KMC_ERR_HIP, "KMC_DEBUG_SYNC: re-sort values not a permutation at " + std::to_string(i));
+    if (i > 0 && (k[i] < k[i - 1] || (k[i] == k[i - 1] && v[i] <= v[i - 1])))
+      return fail(s, KMC_ERR_HIP, "KMC_DEBUG_SYNC: re-sort keys out of order at " + std::to_string(i));
+  }
+  return KMC_OK;
+}
+
 // Home list (kmc_kernels.hip §records): every slot's home cell and position
 // from R, counting sort by cell; hstart = the cells' first home positions.
 static int home_build(kmc_sim* s) {
@@ -545,8 +576,19 @@ static int home_build(kmc_sim* s) {
   const int N = K.N, T = 256;
   HIPCHK(s, hipMemsetAsync(s->hcnt, 0, sizeof(int32_t) * (size_t)(s->ncell + 1), st));
   k_home_count<<<(N + T - 1) / T, T, 0, st>>>(K, d, s->hcnt);
-  size_t tb = s->scan_tmp_bytes;
-  HIPCHK(s, hipcub::DeviceScan::ExclusiveSum(s->scan_tmp, tb, s->hcnt, d.hstart, s->ncell + 1, st));
+  dev_scan(s, s->hcnt, d.hstart, s->ncell + 1, st);
+  if (s->debug_sync) {  // debug: hstart the exclusive scan of the counts
+    const size_t n = (size_t)s->ncell + 1;
+    std::vector<int32_t> c(n), h(n);
+    HIPCHK(s, hipStreamSynchronize(st));
+    HIPCHK(s, hipMemcpy(c.data(), s->hcnt, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+    HIPCHK(s, hipMemcpy(h.data(), d.hstart, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+    int64_t run = 0;
+    for (size_t i = 0; i < n; ++i) {
+      if (h[i] != run) return fail(s, KMC_ERR_HIP, "KMC_DEBUG_SYNC: home scan wrong at " + std::to_string(i));
+      run += c[i];
+    }
+  }
   k_home_place<<<(N + T - 1) / T, T, 0, st>>>(K, d);
   return hipGetLastError() == hipSuccess ? KMC_OK : fail(s, KMC_ERR_HIP, "home_build launch");
 }
@@ -557,18 +599,20 @@ static int resort(kmc_sim* s) {
   const KParams& K = s->K;
   Dev& d = s->d;
   hipStream_t st = s->stream;
-  const int NA = K.NA, NB = K.NB, N = K.N, T = 256;
-  k_slot_keys<<<(N + T - 1) / T, T, 0, st>>>(K, d, s->skeys, s->svals, s->group_sort);
-  const int b0 = s->group_sort ? 0 : 32, b1 = s->group_sort == 2 ? 64 : 32 + s->key_bits;
-  size_t tb = s->sort_tmp_bytes;
-  if (NA > 0)
-    HIPCHK(s, hipcub::DeviceRadixSort::SortPairs(s->sort_tmp, tb, s->skeys, s->skeys2, s->svals, s->svals2, NA, b0,
-                                                 b1, st));
-  tb = s->sort_tmp_bytes;
-  if (NB > 0)
-    HIPCHK(s, hipcub::DeviceRadixSort::SortPairs(s->sort_tmp, tb, s->skeys + NA, s->skeys2 + NA, s->svals + NA,
-                                                 s->svals2 + NA, NB, b0, b1, st));
-  k_slot_inverse<<<(N + T - 1) / T, T, 0, st>>>(K, s->svals2, s->perm, s->newslot);
+  const int N = K.N, T = 256;
+  // packed key widths: unit (reference index < N), cell, complex flag, kind
+  int ob = 0;
+  if (s->group_sort)
+    while ((1ll << ob) < N) ++ob;
+  const int tb = s->group_sort == 2 ? 1 : 0, nbits = ob + s->key_bits + tb + 1;
+  k_slot_keys<<<(N + T - 1) / T, T, 0, st>>>(K, d, s->skeys, s->svals, s->group_sort, ob, s->key_bits);
+  uint64_t* skeys = nullptr;
+  const int32_t* sorted = radix_sort(s, nbits, st, &skeys);
+  if (s->debug_sync) {
+    const int rc = check_sort(s, skeys, sorted);
+    if (rc != KMC_OK) return rc;
+  }
+  k_slot_inverse<<<(N + T - 1) / T, T, 0, st>>>(K, sorted, s->perm, s->newslot);
   reorder(s, s->perm, s->newslot, true);
   k_gather_ids<<<(N + T - 1) / T, T, 0, st>>>(K, d.id_of, s->id_tmp, d.slot_of, s->perm);
   std::swap(d.id_of, s->id_tmp);

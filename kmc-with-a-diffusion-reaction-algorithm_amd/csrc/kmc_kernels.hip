@@ -4461,17 +4461,20 @@ __device__ __forceinline__ uint32_t slot_key(const KParams& P, double x, double 
   return (uint32_t)cell_y(P, y) * (uint32_t)P.ncx + (uint32_t)cell_x(P, x);
 }
 
-// Sort key of slot s: (cell << 32) | unit.  With grouping, a protein takes
-// the cell of its unit's lead (the last step's owner key: a complex's root
-// ligand, a cis dimer's lead receptor, else itself) and the lead's reference
-// index as the low word, so the members of one unit occupy consecutive slots
-// of their kind: the complex kernels then touch a few cache lines per bead
-// row instead of one per member.
-// group 2: members of complexes go after every other protein of their kind
-// (top key bit), so the free units' slots form one dense range: the free
-// proposals then write whole cache lines of R_new, and the complexes' rows
-// are contiguous runs of their own.
-__global__ void k_slot_keys(KParams P, Dev d, uint64_t* keys, int32_t* vals, int group) {
+// Sort key of slot s, packed into the bits the radix sort walks (low to
+// high): the unit (ob bits), the cell (kb bits), the complex flag (group 2),
+// the kind (receptors before ligands: one sort of all N slots leaves each
+// kind in its own range).  With grouping, a protein takes the cell of its
+// unit's lead (the last step's owner key: a complex's root ligand, a cis
+// dimer's lead receptor, else itself) and the lead's reference index as the
+// unit field, so the members of one unit occupy consecutive slots of their
+// kind: the complex kernels then touch a few cache lines per bead row instead
+// of one per member.
+// group 2: members of complexes go after every other protein of their kind,
+// so the free units' slots form one dense range: the free proposals then
+// write whole cache lines of R_new, and the complexes' rows are contiguous
+// runs of their own.
+__global__ void k_slot_keys(KParams P, Dev d, uint64_t* keys, int32_t* vals, int group, int ob, int kb) {
   int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= P.N) return;
   int lead = s, own = d.id_of[s];
@@ -4483,9 +4486,214 @@ __global__ void k_slot_keys(KParams P, Dev d, uint64_t* keys, int32_t* vals, int
     }
   }
   double x = d.cur.P(lead, 1, 1, 0), y = d.cur.P(lead, 1, 1, 1);
-  const uint64_t tail = group == 2 && d.croot[s] >= 0 ? 1ull << 63 : 0ull;
-  keys[s] = tail | (uint64_t)slot_key(P, x, y) << 32 | (uint32_t)(group ? own : 0);
+  const int tb = group == 2 ? 1 : 0;
+  const uint64_t cx = group == 2 && d.croot[s] >= 0 ? 1ull : 0ull;
+  const uint64_t kind = s >= P.NA ? 1ull : 0ull;
+  keys[s] = kind << (ob + kb + tb) | cx << (ob + kb) | (uint64_t)slot_key(P, x, y) << ob |
+            (uint64_t)(group ? (uint32_t)own : 0u);
   vals[s] = s < P.NA ? s : s - P.NA;
+}
+
+// ------------------------------------------------------ radix sort and scan
+// The re-sort's stable LSD radix sort (8-bit digits, as many passes as the
+// packed key has bits) and the exclusive scan of the home list's cell counts.
+// A tile of RS_TILE keys per workgroup: its digit histogram (k_rs_hist),
+// each digit's row of tile counts scanned (k_rs_rows: the tile's first
+// output position within the digit, and the digit's total), then the scatter
+// (k_rs_scatter): each wave ranks its 16 chunks of 64 keys in order — the
+// lanes with the same digit found by 8 ballots, the running count per digit
+// in LDS — the waves' counts are scanned across the workgroup, so equal digits
+// keep their input order (the result equals a stable sort of the whole key),
+// and the tile, placed in LDS in digit order, is written out run by run.  HBM
+// per pass: the keys read twice and the (key, value) pairs written once,
+// ≈ 28 B per slot.
+#define RS_TILE 4096  // keys per workgroup: 256 threads x 16
+#define SCAN_TILE 4096
+
+// lanes of the wave holding the same 8-bit digit as this one (among `live`)
+__device__ __forceinline__ uint64_t rs_peers(uint32_t dg, uint64_t live) {
+  uint64_t m = live;
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    const uint64_t v = __ballot((dg >> b) & 1u);
+    m &= (dg >> b) & 1u ? v : ~v;
+  }
+  return m;
+}
+
+__global__ void __launch_bounds__(256) k_rs_hist(const uint64_t* __restrict__ keys, int n, int shift,
+                                                 int32_t* __restrict__ cnt, int nblk) {
+  __shared__ int h[256];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  const int lane = __lane_id();
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const size_t base = (size_t)blockIdx.x * RS_TILE;
+  for (int j = threadIdx.x; j < RS_TILE; j += 256) {
+    const size_t i = base + j;
+    const bool ok = i < (size_t)n;
+    const uint32_t dg = ok ? (uint32_t)(keys[i] >> shift) & 255u : 0u;
+    const uint64_t pe = rs_peers(dg, __ballot(ok));
+    // one LDS add per digit present in the wave (its lowest lane)
+    if (ok && (pe & lt) == 0) atomicAdd(&h[dg], __popcll(pe));
+  }
+  __syncthreads();
+  cnt[(size_t)threadIdx.x * nblk + blockIdx.x] = h[threadIdx.x];
+}
+
+// exclusive scan over a 256-thread workgroup (sh: 4 ints of LDS); total = the sum
+__device__ __forceinline__ int block_excl_256(int x, int* sh, int& total) {
+  const int lane = __lane_id(), w = threadIdx.x >> 6;
+  int inc = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += t;
+  }
+  if (lane == 63) sh[w] = inc;
+  __syncthreads();
+  int off = 0;
+  total = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = sh[q];
+    off += q < w ? c : 0;
+    total += c;
+  }
+  __syncthreads();  // (sh reusable)
+  return off + inc - x;
+}
+// per digit: the exclusive scan of its row of tile counts, and its total
+__global__ void __launch_bounds__(256) k_rs_rows(int32_t* __restrict__ cnt, int nblk, int32_t* __restrict__ tot) {
+  __shared__ int sh[4];
+  int32_t* row = cnt + (size_t)blockIdx.x * nblk;
+  int carry = 0;
+  for (int b0 = 0; b0 < nblk; b0 += 256) {
+    const int i = b0 + (int)threadIdx.x;
+    const int x = i < nblk ? row[i] : 0;
+    int t;
+    const int e = block_excl_256(x, sh, t);
+    if (i < nblk) row[i] = carry + e;
+    carry += t;
+  }
+  if (threadIdx.x == 0) tot[blockIdx.x] = carry;
+}
+
+// The tile's keys ranked (stable) and placed in LDS in digit order, then
+// written out run by run: consecutive threads store consecutive positions of
+// a digit's output range.
+__global__ void __launch_bounds__(256) k_rs_scatter(const uint64_t* __restrict__ kin, const int32_t* __restrict__ vin,
+                                                    uint64_t* __restrict__ kout, int32_t* __restrict__ vout, int n,
+                                                    int shift, const int32_t* __restrict__ cnt,
+                                                    const int32_t* __restrict__ tot, int nblk) {
+  __shared__ int wc[4][256];
+  __shared__ int gb[256], ts[256], sh[4];
+  __shared__ uint64_t sk[RS_TILE];
+  __shared__ int32_t sv[RS_TILE];
+  const int lane = __lane_id(), w = threadIdx.x >> 6, t = threadIdx.x;
+  for (int i = t; i < 4 * 256; i += 256) (&wc[0][0])[i] = 0;
+  {
+    int all;
+    const int db = block_excl_256(tot[t], sh, all);  // the digit's first output position
+    gb[t] = db + cnt[(size_t)t * nblk + blockIdx.x];
+  }
+  __syncthreads();
+  const size_t base = (size_t)blockIdx.x * RS_TILE + (size_t)w * (RS_TILE / 4);
+  const uint64_t lt = (1ull << lane) - 1ull;
+  constexpr int C = RS_TILE / 256;
+  uint64_t k[C];
+  int32_t v[C], r[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const size_t i = base + (size_t)c * 64 + lane;
+    k[c] = i < (size_t)n ? kin[i] : 0ull;
+    v[c] = i < (size_t)n ? vin[i] : 0;
+  }
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const bool ok = base + (size_t)c * 64 + lane < (size_t)n;
+    const uint32_t dg = (uint32_t)(k[c] >> shift) & 255u;
+    const uint64_t pe = rs_peers(dg, __ballot(ok));
+    // (a wave's LDS operations complete in order: this chunk's read sees the
+    // previous chunk's update)
+    const int prior = ok ? wc[w][dg] : 0;
+    r[c] = prior + __popcll(pe & lt);
+    if (ok && (pe & ~lt & ~(1ull << lane)) == 0) wc[w][dg] = prior + __popcll(pe);  // the group's last lane
+  }
+  __syncthreads();
+  {  // the waves' counts of digit t -> offsets across the waves; the tile's digit starts
+    int run = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = wc[q][t];
+      wc[q][t] = run;
+      run += c;
+    }
+    int all;
+    ts[t] = block_excl_256(run, sh, all);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    if (base + (size_t)c * 64 + lane >= (size_t)n) continue;
+    const uint32_t dg = (uint32_t)(k[c] >> shift) & 255u;
+    const int lp = ts[dg] + wc[w][dg] + r[c];
+    sk[lp] = k[c];
+    sv[lp] = v[c];
+  }
+  __syncthreads();
+  const int m = (int)min((size_t)RS_TILE, (size_t)n - (size_t)blockIdx.x * RS_TILE);
+  for (int j = t; j < m; j += 256) {
+    const uint64_t key = sk[j];
+    const uint32_t dg = (uint32_t)(key >> shift) & 255u;
+    const int pos = gb[dg] + j - ts[dg];
+    kout[pos] = key;
+    vout[pos] = sv[j];
+  }
+}
+
+// exclusive scan, three launches: tile sums, their scan, the tiles' scans
+__global__ void __launch_bounds__(256) k_scan_part(const int32_t* __restrict__ in, int n, int32_t* __restrict__ part) {
+  __shared__ int sh[4];
+  const size_t base = (size_t)blockIdx.x * SCAN_TILE + (size_t)threadIdx.x * (SCAN_TILE / 256);
+  int x = 0;
+#pragma unroll
+  for (int j = 0; j < SCAN_TILE / 256; ++j)
+    if (base + j < (size_t)n) x += in[base + j];
+  int tot;
+  (void)block_excl_256(x, sh, tot);
+  if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+__global__ void __launch_bounds__(256) k_scan_top(int32_t* part, int nb) {
+  __shared__ int sh[4];
+  int carry = 0;
+  for (int b0 = 0; b0 < nb; b0 += 256) {
+    const int i = b0 + (int)threadIdx.x;
+    const int x = i < nb ? part[i] : 0;
+    int tot;
+    const int e = block_excl_256(x, sh, tot);
+    if (i < nb) part[i] = carry + e;
+    carry += tot;
+  }
+}
+__global__ void __launch_bounds__(256) k_scan_down(const int32_t* in, int32_t* out, int n,
+                                                   const int32_t* __restrict__ part) {
+  __shared__ int sh[4];
+  constexpr int J = SCAN_TILE / 256;
+  const size_t base = (size_t)blockIdx.x * SCAN_TILE + (size_t)threadIdx.x * J;
+  int x[J], s = 0;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    x[j] = base + j < (size_t)n ? in[base + j] : 0;
+    s += x[j];
+  }
+  int tot;
+  int run = part[blockIdx.x] + block_excl_256(s, sh, tot);
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    if (base + j < (size_t)n) out[base + j] = run;
+    run += x[j];
+  }
 }
 
 // ---------------------------------------------------------------- home list
