@@ -3515,7 +3515,10 @@ __global__ void k_col_dense(KParams P, Dev d) {
   for (uint32_t b = blockIdx.x; b < nd; b += gridDim.x) dense_block(P, d, d.dense[b], tag);
 }
 
-__global__ void k_col_exact(KParams P, Dev d) {
+#ifndef COLX_WAVES  // minimum waves per SIMD of k_col_exact (4: the 128-VGPR cap an unbounded kernel gets)
+#define COLX_WAVES 4
+#endif
+__global__ void __launch_bounds__(256, COLX_WAVES) k_col_exact(KParams P, Dev d) {
   const uint32_t tag = (d.ctl->step & 0x3fffffffu) << 2;
   __shared__ uint32_t pre[NSHARD + 1];
 #if !DENSE_KERNEL
