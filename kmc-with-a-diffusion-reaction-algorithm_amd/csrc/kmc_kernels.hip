@@ -3678,6 +3678,9 @@ __device__ __forceinline__ void rej_copy(const KParams& P, const Dev& d, int m, 
 // of k_match, which move receptors in R_new that a revert must restore first — DESIGN.md §8)
 #error "REJ_SIDE is wrong by design"
 #endif
+#ifndef REJ_ROWMAJOR  // the (member, row) copies of a unit's lanes ordered row-major
+#define REJ_ROWMAJOR 1
+#endif
 #ifndef REJ_UNROLL  // rejected units whose lookups a lane group has in flight at once
 #define REJ_UNROLL 1
 #endif
@@ -3721,7 +3724,14 @@ __device__ __forceinline__ void rej_commit(const KParams& P, const Dev& d, uint3
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       auto member = [&](int k) { return kind[u] == U_COMPLEX ? d.members[off[u] + k] : (k ? q[u] : sl[u]); };
+#if REJ_ROWMAJOR
+      // row-major over the members: neighbouring lanes copy one row of
+      // neighbouring members, which the grouped slot order puts in consecutive
+      // slots — the same cache line of the row's 64-slot block
+      for (int e = lane; e < nm[u] * ROWS_A; e += REJ_LANES) rej_copy(P, d, member(e % nm[u]), e / nm[u]);
+#else
       for (int e = lane; e < nm[u] * ROWS_A; e += REJ_LANES) rej_copy(P, d, member(e / ROWS_A), e % ROWS_A);
+#endif
     }
   }
 }
