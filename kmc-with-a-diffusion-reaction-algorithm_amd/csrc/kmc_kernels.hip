@@ -1788,6 +1788,9 @@ __device__ __forceinline__ void cx_row_beads(bool lig, int row, int& b0, int& b1
   b1 = (2 * h + 1) * nk + kk;
 }
 
+#ifndef CX_ROWMAJOR  // staged complexes' (member, row) loads and stores ordered row-major (A/B,
+#define CX_ROWMAJOR 0    // profiles/r05/complex/r6u_*: k_complex_heavy at C5 428 -> 447 us, C3 52.0 -> 53.7)
+#endif
 #ifndef CXB_IT  // (A/B: 3 -> 6, every row of a 16-member complex in one round: C5 437 -> 426 us, profiles/r05/complex/r6d_*)
 #define CXB_IT 6
 #endif
@@ -1801,9 +1804,13 @@ __device__ __forceinline__ void cx_load_beads(const Dev& d, CxLds* L, int csize,
   int qi[IT];  // member | row << 8 | ligand << 16, or -1
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
+#if CX_ROWMAJOR
+    const int e = e0 + lane + it * 64, row = e / csize, q = e - row * csize;
+#else
     const int e = e0 + lane + it * 64, q = e / ROWS_A, row = e - q * ROWS_A;
+#endif
     qi[it] = -1;
-    if (q < csize) {
+    if (q < csize && row < ROWS_A) {
       const int m = L->slot[q];
       if (m < NA) {
         v[it] = d.nxt.A2(m, row);
@@ -1837,7 +1844,11 @@ __device__ __forceinline__ void cx_load_beads(const Dev& d, CxLds* L, int csize,
 // order (cluster.log, main.cpp:2291-2305)
 __device__ __forceinline__ void cx_write_back(const Dev& d, CxLds* L, int* grow, int csize, int nB, int NA, int lane) {
   for (int e = lane; e < csize * ROWS_A; e += 64) {
+#if CX_ROWMAJOR
+    const int row = e / csize, q = e - row * csize, m = L->slot[q];
+#else
     const int q = e / ROWS_A, row = e - q * ROWS_A, m = L->slot[q];
+#endif
     const bool lig = m >= NA;
     if (lig && row >= ROWS_B) continue;
     int b0, b1;
