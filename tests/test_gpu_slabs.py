@@ -6,9 +6,12 @@ record and the full-state hash must equal the single-handle run of the same
 trajectory (itself bit-identical to the keyed oracle, test_gpu_parity.py),
 while units of different slabs collide and bond across the cuts."""
 import importlib
+import os
+import socket
 
 import numpy as np
 import pytest
+import torch.multiprocessing as mp
 
 from _kmc import DENSE, PKG, engine, params, workloads
 
@@ -71,3 +74,39 @@ def test_slabs_c2_window(G):
     s, _ = compare(p, st, G, 100)
     print(f"C2 G={G}: {s}")
     assert s["verified"] > 0 and s["owned"] < p.n_a + p.n_b, s
+
+
+def _gloo_gpu_worker(rank, world, port, out, steps):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    p = params(n_a=20000, n_b=7000, seed=9, box_x=14000.0, box_y=14000.0, box_z=250.0, **RATES)
+    st = engine.host_init_random(p)
+    me = slabs.SlabRank(p, rank, slabs.TorchComm(), window_handle, gather_every=steps)
+    me.start(st)
+    recs = np.concatenate([me.step() for _ in range(steps)])
+    if rank == 0:
+        np.savez(out, recs=recs, hash=np.uint64(engine.state_hash(p, me.last_global)), xcol=me.stats["xcol"],
+                 xbond=me.stats["xbond"], verified=me.stats["verified"])
+    me.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_slabs_two_processes_gpu(tmp_path):
+    # one rank per process, each with its own libkmc handle on the device and
+    # the exchange over torch.distributed (gloo): the one-process-per-GPU shape
+    # of the decomposed mode, here with both ranks on one device
+    steps = 200
+    out = str(tmp_path / "slabs.npz")
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    mp.spawn(_gloo_gpu_worker, args=(2, port, out, steps), nprocs=2, join=True)
+    got = np.load(out)
+    p = params(n_a=20000, n_b=7000, seed=9, box_x=14000.0, box_y=14000.0, box_z=250.0, **RATES)
+    ref, ref_h = single_gpu(p, engine.host_init_random(p), steps)
+    assert np.array_equal(got["recs"], ref)
+    assert int(got["hash"]) == int(ref_h[-1])
+    assert int(got["xcol"]) > 0 and int(got["verified"]) > 0
