@@ -3104,6 +3104,9 @@ __device__ __forceinline__ void item_ranges(const KParams& P, const TileLds& T, 
 // (16 records = 128 B apart mod 256 B).  Records base + 4·lane + wv (the
 // round-robin order before) put a group's lanes 64 B apart: 4-way conflicts
 // on every owner read (SQ_LDS_BANK_CONFLICT, profiles/r05/ab_walk).
+#ifndef WALK_MAXSEL  // the owner's range of a pair chosen by one unsigned max over its packed words (A/B,
+#define WALK_MAXSEL 0    // profiles/r05/ab_walk/r7a_*: k_pair_scan 112.3 -> 113.0 us at C3, 1232 -> 1237 at C5)
+#endif
 #define PAIR_THREADS 256  // threads of a k_pair_scan workgroup (tile_walk's wave count)
 __device__ __forceinline__ int walk_item(int base, int lane, int wv, int nw) {
 #if WALK_PERM
@@ -3139,7 +3142,11 @@ __device__ __forceinline__ void tile_walk(const TileGeo& G, const TileLds& T, ui
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
       const int len = item ? r1[k] - r0[k] : 0;
+#if WALK_MAXSEL
+      pk[k] = len > 0 ? (uint32_t)r0[k] | (uint32_t)tot << 16 : 0u;  // (an empty range never wins the max)
+#else
       pk[k] = (uint32_t)(item ? r0[k] : 0) | (uint32_t)tot << 16;
+#endif
       tot += len;
     }
 #if WALK_BITS
@@ -3185,13 +3192,24 @@ __device__ __forceinline__ void tile_walk(const TileGeo& G, const TileLds& T, ui
         before += __popc(m.x) + __popc(m.y);
         const int q = j + lane, oa = o << 2;
         const int eo = __builtin_amdgcn_ds_bpermute(oa, ew);
-        uint32_t sel = (uint32_t)__builtin_amdgcn_ds_bpermute(oa, (int)pk[0]);
         const int t = q - (eo & 0xffffff);
+#if WALK_MAXSEL
+        // the last non-empty range starting at or before pair t: its packed
+        // word (start | pairs before << 16) is the largest below (t + 1) << 16,
+        // and x - (t + 1) << 16 (mod 2^32) orders those above every other word
+        const uint32_t T1 = (uint32_t)(t + 1) << 16;
+        uint32_t mx = (uint32_t)__builtin_amdgcn_ds_bpermute(oa, (int)pk[0]) - T1;
+#pragma unroll
+        for (int k = 1; k < 6; ++k) mx = max(mx, (uint32_t)__builtin_amdgcn_ds_bpermute(oa, (int)pk[k]) - T1);
+        const uint32_t sel = mx + T1;
+#else
+        uint32_t sel = (uint32_t)__builtin_amdgcn_ds_bpermute(oa, (int)pk[0]);
 #pragma unroll
         for (int k = 1; k < 6; ++k) {
           const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute(oa, (int)pk[k]);
           if ((int)(v >> 16) <= t) sel = v;
         }
+#endif
 #if WALK_STRIDE
         if (q < wtot) chk(walk_item(base, (int)((uint32_t)eo >> 24), wv, nw), (int)(sel & 0xffffu) + t - (int)(sel >> 16));
 #else
