@@ -111,8 +111,37 @@ class TorchComm:
         return out
 
     def alltoall(self, rank: int, objs: list) -> list:
-        allv = self.allgather(rank, objs)
-        return [allv[src][rank] for src in range(self.world)]
+        """objs[r] to rank r; returns the messages from every rank.  Over gloo
+        each message goes only to its destination (sizes all-gathered, then
+        point-to-point); other backends all-gather every message."""
+        if self.dist.get_backend() != "gloo":
+            allv = self.allgather(rank, objs)
+            return [allv[src][rank] for src in range(self.world)]
+        import pickle
+
+        import torch
+
+        W = self.world
+        data = [b"" if r == rank or objs[r] is None else pickle.dumps(objs[r], protocol=5) for r in range(W)]
+        sizes = [torch.zeros(W, dtype=torch.int64) for _ in range(W)]
+        self.dist.all_gather(sizes, torch.tensor([len(x) for x in data], dtype=torch.int64))
+        reqs, bufs = [], {}
+        for r in range(W):
+            if r == rank:
+                continue
+            if data[r]:
+                reqs.append(self.dist.isend(torch.frombuffer(bytearray(data[r]), dtype=torch.uint8), r))
+            n = int(sizes[r][rank])
+            if n:
+                bufs[r] = torch.empty(n, dtype=torch.uint8)
+                reqs.append(self.dist.irecv(bufs[r], r))
+        for q in reqs:
+            q.wait()
+        out = [None] * W
+        out[rank] = objs[rank]
+        for r, b in bufs.items():
+            out[r] = pickle.loads(b.numpy().tobytes())  # (a peer rank's own message)
+        return out
 
 
 def run_threads(world: int, fn: Callable[[int], object]) -> list:
