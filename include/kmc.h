@@ -188,6 +188,9 @@ int kmc_host_append_cluster_log(const kmc_params* p, int64_t step, const int32_t
                                 const char* path);
 /* bond-link consistency + rigid-body extent bound; KMC_OK or an error code */
 int kmc_host_validate(const kmc_params* p, const kmc_state_view* v);
+/* the arguments kmc_dd_set_state checks first: gid[0..n) increasing and in
+ * [0, INT32_MAX), own[i] 0 or 1; KMC_OK or KMC_ERR_ARG */
+int kmc_host_dd_check(int32_t n, const int32_t* gid, const uint8_t* own);
 
 /* Domain decomposition of ONE trajectory over several handles (SURVEY.md
  * §8(f).4; the host driver is slabs.py).  The reference has no
@@ -225,6 +228,70 @@ int kmc_dd_import(kmc_sim* s, int32_t n, const int32_t* ids, const double* beads
 int kmc_dd_drift(kmc_sim* s, double* max_dx);
 int kmc_dd_jumpers(kmc_sim* s, double S, int32_t cap, int32_t* ids, double* xs, int32_t* n);
 int kmc_dd_counters(kmc_sim* s, int64_t* out);
+
+/* The halo exchange on device memory (the per-step path of slabs.py; the
+ * host-buffer export / import above stay for diagnostics).  One exchanged
+ * row is KMC_DD_ROW bytes: 48 doubles (kmc_dd_export's bead order) then 8
+ * int32 (kmc_dd_export's fields) whose links are GLOBAL reference index + 1
+ * (0 = none), so a row means the same thing in every window.
+ *   kmc_dd_plan    once per partition (and after an ownership change):
+ *                  send_ids[n_send] the local ids whose rows this window
+ *                  sends, grouped by destination; recv_ids[n_recv] the local
+ *                  ids of the rows it receives, grouped by source, each group
+ *                  in its source's send order; own[N] replaces the ownership
+ *                  of kmc_dd_set_state; band[N] = 1 for the halo proteins
+ *                  whose end-of-step state must equal their owner's.  Sent
+ *                  proteins must be owned, received ones not.
+ *   kmc_dd_pack    the end-of-step rows of send_ids into device memory dst
+ *                  (n_send rows; NULL: the handle's own send buffer,
+ *                  kmc_dd_send_buffer).  Returns after the stream drained.
+ *   kmc_dd_unpack  rows [first, first + n) of the receive plan from device
+ *                  memory src (another handle's send buffer on this device,
+ *                  or a collective's receive buffer), enqueued on the
+ *                  handle's stream: each row's links go through a binary
+ *                  search of the window's global indices; a link to a
+ *                  protein the window does not hold is cut with its status;
+ *                  the row overwrites this handle's own result and the
+ *                  differences are counted.
+ *   kmc_dd_finish  waits for the unpacks and returns the step's report: band
+ *                  rows that differed or had a link cut (bad; > 0 means the
+ *                  step must be redone from a wider partition), rows that
+ *                  differed, rows whose status / links differed; the owned
+ *                  proteins more than S (periodic x) from their x at
+ *                  kmc_dd_set_state (n_jump, the first KMC_DD_JCAP listed as
+ *                  local id + x); the bonds formed since the last finish
+ *                  between an owned and a halo protein (n_xb, the first
+ *                  KMC_DD_XCAP as local id pairs); kmc_dd_counters' values.
+ *   kmc_dd_cut_count  how many of ids[n] had a link cut at the last unpack
+ *                  (their unit is not held whole by this window).
+ * A decomposed window takes no chunk snapshot (the slab driver keeps the
+ * checkpoint): a kmc_step that raises a device error leaves the window's
+ * state undefined and returns the error; after a list overflow
+ * (KMC_ERR_CAPACITY) the lists have already been doubled —
+ * kmc_list_growth / kmc_set_list_growth carry that size to the handle the
+ * driver rebuilds. */
+#define KMC_DD_ROW 416
+#define KMC_DD_JCAP 256
+#define KMC_DD_XCAP 64
+typedef struct kmc_dd_report {
+  int64_t xcol, xbond;
+  int32_t bad, differed, links, n_jump, n_xb, reserved;
+  int32_t jump_id[KMC_DD_JCAP];
+  double jump_x[KMC_DD_JCAP];
+  int32_t xb[KMC_DD_XCAP][2];
+} kmc_dd_report;
+int kmc_dd_plan(kmc_sim* s, int32_t n_send, const int32_t* send_ids, int32_t n_recv, const int32_t* recv_ids,
+                const uint8_t* own, const uint8_t* band);
+int kmc_dd_pack(kmc_sim* s, void* dst);
+void* kmc_dd_send_buffer(kmc_sim* s);
+int kmc_dd_unpack(kmc_sim* s, const void* src, int32_t first, int32_t n);
+int kmc_dd_finish(kmc_sim* s, double S, kmc_dd_report* out);
+int kmc_dd_cut_count(kmc_sim* s, int32_t n, const int32_t* ids, int32_t* count);
+
+/* Output-list capacities as 2^level times their defaults (kmc_step doubles
+ * them itself after an overflow, up to level 6). */
+int kmc_list_growth(const kmc_sim* s);
+int kmc_set_list_growth(kmc_sim* s, int32_t level);
 
 /* Diagnostics: the portable math of kmc_math.h evaluated on the host and on
  * the device (op 0 sin, 1 cos, 2 atan2(x,y), 3 acos, 4 sqrt, 5 x/y, 6 round)

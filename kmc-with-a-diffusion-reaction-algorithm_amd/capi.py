@@ -128,6 +128,39 @@ class StateView(C.Structure):
     ]
 
 
+DD_ROW = 416     # KMC_DD_ROW: one exchanged protein (48 doubles + 8 int32)
+DD_JCAP = 256    # KMC_DD_JCAP
+DD_XCAP = 64     # KMC_DD_XCAP
+
+
+class DDReport(C.Structure):
+    """kmc_dd_report — one slab window's checks after a step's halo exchange."""
+
+    _fields_ = [
+        ("xcol", C.c_int64),
+        ("xbond", C.c_int64),
+        ("bad", C.c_int32),
+        ("differed", C.c_int32),
+        ("links", C.c_int32),
+        ("n_jump", C.c_int32),
+        ("n_xb", C.c_int32),
+        ("reserved", C.c_int32),
+        ("jump_id", C.c_int32 * DD_JCAP),
+        ("jump_x", C.c_double * DD_JCAP),
+        ("xb", (C.c_int32 * 2) * DD_XCAP),
+    ]
+
+    def jumpers(self):
+        """(local ids, x) of the listed jumpers."""
+        n = min(self.n_jump, DD_JCAP)
+        return (np.ctypeslib.as_array(self.jump_id)[:n].copy(), np.ctypeslib.as_array(self.jump_x)[:n].copy())
+
+    def cross_bonds(self) -> np.ndarray:
+        """[n, 2] local ids of the listed cross-slab bonds."""
+        n = min(self.n_xb, DD_XCAP)
+        return np.ctypeslib.as_array(self.xb).reshape(DD_XCAP, 2)[:n].copy()
+
+
 def default_params(**overrides) -> Params:
     """Reference defaults, main.cpp:39-99 (mirrors kmc_params_default)."""
     p = Params()

@@ -85,8 +85,22 @@ struct Ctl {
   uint32_t dd_xcol, dd_xbond;
 };
 
+// One slab window's per-step exchange report (kmc_dd_finish; the layout of
+// kmc_dd_report in include/kmc.h): the unpacks count the checks, k_dd_jumpers
+// lists the jumpers, the matching lists the cross-slab bonds.  xcol / xbond
+// are filled on the host from Ctl.
+#define DD_JCAP 256
+#define DD_XCAP 64
+struct DDRep {
+  int64_t xcol, xbond;
+  int32_t bad, differed, links, n_jump, n_xb, reserved;
+  int32_t jump_id[DD_JCAP];
+  double jump_x[DD_JCAP];
+  int32_t xb[DD_XCAP][2];
+};
+
 enum : uint32_t {
-  ERR_EDGES = 1u,       // an output list / reaction edge buffer full (kmc_step grows them and replays)
+  ERR_EDGES = 1u,      // an output list / reaction edge buffer full (kmc_step grows them and replays)
   ERR_GEOMETRY = 2u,    // rigid-body extent bound violated
   ERR_RESOLVE = 4u,     // collision resolution did not converge
   ERR_ALIGN = 8u,       // alignment repeat guard

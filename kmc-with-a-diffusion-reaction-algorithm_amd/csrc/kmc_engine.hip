@@ -114,6 +114,14 @@ struct kmc_sim {
   int32_t* dd_ints = nullptr;
   uint8_t* dd_flags = nullptr;
   int32_t dd_cap = 0;
+  // the device-resident exchange (kmc_dd_plan / pack / unpack / finish)
+  DDRep* dd_rep = nullptr;          // the step's report, filled by the kernels
+  uint8_t* dd_band = nullptr;       // [N] band flags of the plan
+  uint8_t* dd_cut = nullptr;        // [N] a link of the protein was cut at the last unpack
+  int32_t* dd_send_ids = nullptr;   // [dd_send_cap]
+  int32_t* dd_recv_ids = nullptr;   // [dd_recv_cap]
+  unsigned char* dd_sendbuf = nullptr;  // [dd_send_cap rows]
+  int32_t dd_n_send = 0, dd_n_recv = 0, dd_send_cap = 0, dd_recv_cap = 0;
 };
 
 namespace {
@@ -335,6 +343,7 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   Dev& d = s->d;
   d.cur.NA = d.nxt.NA = NA;
   d.cur.NB = d.nxt.NB = NB;
+  d.nkeys = (uint32_t)N;
   int rc = KMC_OK;
   rc |= dalloc(s, &d.cur.a, 48 * bead_slots(NA));
   rc |= dalloc(s, &d.nxt.a, 48 * bead_slots(NA));
@@ -1101,7 +1110,10 @@ int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out) {
   while (done < nsteps) {
     const int64_t n = std::min(chunk, nsteps - done);
     int rc = KMC_OK;
-    if (!s->snap_valid || s->step_done + n - s->snap_step > s->snap_span) {
+    // a decomposed window takes no snapshot: every step's import changes its
+    // state (a replay from a snapshot would miss the imports), and the slab
+    // driver keeps the checkpoint it rolls back to
+    if (!s->K.dd && (!s->snap_valid || s->step_done + n - s->snap_step > s->snap_span)) {
       rc = snapshot(s, false);
       if (rc != KMC_OK) return rc;
       s->snap_valid = true;
@@ -1118,6 +1130,22 @@ int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out) {
       // dropped entries, so their bits may be consequences
       const uint32_t cause = s->ctl_host->err_first;
       const int64_t bad = (int64_t)s->ctl_host->err_step;
+      if (s->K.dd) {
+        // no snapshot to undo to: the window's state is lost.  A list
+        // overflow alone doubles the lists first, so that the handle the
+        // driver rebuilds (kmc_list_growth) runs the step with room
+        const bool grow = (cause & ~ERR_EDGES) == 0;
+        if (grow && s->grow < 6) {
+          s->grow += 1;
+          if (alloc_lists(s) != KMC_OK) return fail(s, KMC_ERR_HIP, "growing the output lists failed");
+        }
+        s->have_state = false;
+        s->clusters_valid = false;
+        char m[200];
+        snprintf(m, sizeof m, "dd: device error bits 0x%x at step %lld; the window's state is lost (list growth 2^%d)",
+                 err, (long long)bad, s->grow);
+        return fail(s, grow ? KMC_ERR_CAPACITY : (cause & ERR_GEOMETRY) ? KMC_ERR_GEOMETRY : KMC_ERR_CAPACITY, m);
+      }
       // undo to the snapshot, then replay the steps between it and this
       // chunk (already returned by earlier calls: same trajectory, keyed
       // draws) without output
@@ -1437,6 +1465,133 @@ __global__ void k_dd_jumpers(KParams P, Dev d, double S, int cap, int32_t* ids, 
   }
 }
 
+// the same list into the step's report (kmc_dd_finish)
+__global__ void k_dd_jumpers_rep(KParams P, Dev d, double S) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P.N) return;
+  const int r = d.id_of[p];
+  if (!d.dd_own[r]) return;
+  const double x = d.cur.P(p, 1, 1, 0);
+  double dx = x - d.dd_x0[r];
+  dx = dx - P.box_x * kmcm::round_(dx / P.box_x);
+  if (!(kmcm::fabs_(dx) > S)) return;
+  const uint32_t k = atomicAdd((uint32_t*)&d.dd_rep->n_jump, 1u);
+  if (k < DD_JCAP) {
+    d.dd_rep->jump_id[k] = r;
+    d.dd_rep->jump_x[k] = x;
+  }
+}
+
+// Rows of the exchange (kmc_dd_pack): row i = the end-of-step state of local
+// protein ids[i] — 48 doubles, then 8 ints at byte 384 with the links as
+// global reference index + 1.  One thread per double / int of a row.
+__global__ void k_dd_pack(KParams P, Dev d, int n, const int32_t* ids, unsigned char* rows) {
+  const int NA = P.NA, NB = P.NB;
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (size_t)n * 56) return;
+  const int i = (int)(t / 56), e = (int)(t % 56), slot = d.slot_of[ids[i]];
+  unsigned char* row = rows + (size_t)i * KMC_DD_ROW;
+  if (e < 48) {
+    const int bead = e / 3, c = e % 3;
+    double v = 0.0;
+    if (slot < NA) v = d.cur.A(slot, bead / 4 + 1, bead % 4 + 1, c);
+    else if (e < 24) v = d.cur.B(slot - NA, bead / 2 + 1, bead % 2 + 1, c);
+    reinterpret_cast<double*>(row)[e] = v;
+    return;
+  }
+  const int f = e - 48;
+  int v = 0;
+  bool link = false;
+  if (slot < NA) {
+    if (f < 5) v = d.a_int[(size_t)f * NA + slot];
+    link = f == 2 || f == 4;
+  } else {
+    v = d.b_int[(size_t)f * NB + (slot - NA)];
+    link = f >= 4;
+  }
+  if (link && v > 0) v = d.gid[d.id_of[v - 1]] + 1;
+  reinterpret_cast<int32_t*>(row + 384)[f] = v;
+}
+
+// The owners' rows over this window's halo copies (kmc_dd_unpack): one wave
+// per row, lanes 0..47 the doubles, 48..55 the ints.  A link (global index +
+// 1) is found in the window by a binary search of gid (increasing); a link to
+// a protein the window does not hold is cut, clearing the status it carries
+// (receptor nei2 -> st2 and nei4, nei3 -> st3; ligand nei j -> st j), as the
+// window was cut when it was set.  The row overwrites the window's own result;
+// rows that differed are counted, and band rows that differed or had a link
+// cut make the step's check fail (DDRep::bad).
+__global__ __launch_bounds__(256) void k_dd_unpack(KParams P, Dev d, int n, const int32_t* ids,
+                                                   const unsigned char* rows, const uint8_t* band, uint8_t* cut) {
+  const int NA = P.NA, NB = P.NB, N = P.N;
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;  // a whole wave
+  const int r = ids[i], slot = d.slot_of[r];
+  const bool rec = slot < NA;
+  const unsigned char* row = rows + (size_t)i * KMC_DD_ROW;
+  bool dif = false, difi = false, lost = false;
+  double* dst = nullptr;
+  double v = 0.0;
+  if (lane < 48) {
+    const int bead = lane / 3, c = lane % 3;
+    if (rec) dst = &d.cur.A(slot, bead / 4 + 1, bead % 4 + 1, c);
+    else if (lane < 24) dst = &d.cur.B(slot - NA, bead / 2 + 1, bead % 2 + 1, c);
+    if (dst) {
+      v = reinterpret_cast<const double*>(row)[lane];
+      dif = __double_as_longlong(*dst) != __double_as_longlong(v);
+    }
+  }
+  const int f = lane - 48;
+  int32_t* dsti = nullptr;
+  int vi = 0;
+  if (f >= 0 && f < 8) {
+    bool link;
+    if (rec) {
+      if (f < 5) dsti = &d.a_int[(size_t)f * NA + slot];
+      link = f == 2 || f == 4;
+    } else {
+      dsti = &d.b_int[(size_t)f * NB + (slot - NA)];
+      link = f >= 4;
+    }
+    vi = reinterpret_cast<const int32_t*>(row + 384)[f];
+    if (link && vi > 0) {
+      const int g = vi - 1;
+      int lo = 0, hi = N;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (d.gid[mid] < g) lo = mid + 1;
+        else hi = mid;
+      }
+      if (lo < N && d.gid[lo] == g) {
+        vi = d.slot_of[lo] + 1;
+      } else {
+        vi = 0;
+        lost = true;
+      }
+    }
+  }
+  const uint32_t lostf = (uint32_t)(__ballot(lost) >> 48) & 0xffu;  // bit f: link field f was cut
+  if (dsti) {
+    if (rec) {
+      if ((f == 0 || f == 3) && (lostf & (1u << 2))) vi = 0;
+      if (f == 1 && (lostf & (1u << 4))) vi = 0;
+    } else if (f < 4 && (lostf & (1u << (4 + f)))) {
+      vi = 0;
+    }
+    difi = *dsti != vi;
+    if (difi) *dsti = vi;
+  }
+  if (dif) *dst = v;
+  const bool anyb = __ballot(dif) != 0, anyi = __ballot(difi) != 0;
+  if (lane == 0) {
+    cut[r] = lostf != 0;
+    if (anyb || anyi) atomicAdd(&d.dd_rep->differed, 1);
+    if (anyi) atomicAdd(&d.dd_rep->links, 1);
+    if (band[r] && (anyb || anyi || lostf)) atomicAdd(&d.dd_rep->bad, 1);
+  }
+}
+
 extern "C" {
 
 static int dd_stage(kmc_sim* s, int32_t n) {
@@ -1457,19 +1612,26 @@ int kmc_dd_set_state(kmc_sim* s, const kmc_state_view* v, const int32_t* gid, co
                      const int32_t* ctl5) {
   if (!s || !v || !gid || !own || !ctl5) return KMC_ERR_ARG;
   const int NA = s->p.n_a, NB = s->p.n_b, N = NA + NB;
-  // the local numbering must be monotone in the global one (receptors, then
-  // ligands): every order the step takes (unit keys, BFS roots, the greedy
-  // reactions) then equals the global order restricted to the window
-  for (int i = 1; i < N; ++i)
-    if (gid[i] <= gid[i - 1]) return fail(s, KMC_ERR_ARG, "dd: global indices not increasing");
-  if (N > 0 && gid[0] < 0) return fail(s, KMC_ERR_ARG, "dd: negative global index");
+  // monotone local numbering, global indices in range, ownership 0 / 1
+  {
+    const int rc = kmch_host::dd_check(N, gid, own, &s->err);
+    if (rc != KMC_OK) return rc;
+  }
   if (!s->dd_gid) {
     int rc = dalloc(s, &s->dd_gid, (size_t)N);
     rc |= dalloc(s, &s->dd_own, (size_t)N);
     rc |= dalloc(s, &s->dd_x0, (size_t)N);
     rc |= dalloc(s, &s->dd_scratch, 2);
+    rc |= dalloc(s, &s->dd_rep, 1);
+    rc |= dalloc(s, &s->dd_band, (size_t)N);
+    rc |= dalloc(s, &s->dd_cut, (size_t)N);
     if (rc != KMC_OK) return fail(s, KMC_ERR_HIP, "dd buffers");
   }
+  HIPCHK(s, hipMemsetAsync(s->dd_rep, 0, sizeof(DDRep), s->stream));
+  HIPCHK(s, hipMemsetAsync(s->dd_band, 0, (size_t)N, s->stream));
+  HIPCHK(s, hipMemsetAsync(s->dd_cut, 0, (size_t)N, s->stream));
+  HIPCHK(s, hipStreamSynchronize(s->stream));
+  s->dd_n_send = s->dd_n_recv = 0;
   std::vector<double> x0((size_t)N);
   for (int i = 0; i < NA; ++i) x0[i] = v->ra[i];  // bead [1][1], x: row 0 of the host layout
   for (int b = 0; b < NB; ++b) x0[NA + b] = v->rb[b];
@@ -1504,6 +1666,7 @@ int kmc_dd_set_state(kmc_sim* s, const kmc_state_view* v, const int32_t* gid, co
   s->d.gid = s->dd_gid;
   s->d.dd_own = s->dd_own;
   s->d.dd_x0 = s->dd_x0;
+  s->d.dd_rep = s->dd_rep;
   int rc = set_state_impl(s, v);
   if (rc != KMC_OK) return rc;
   // the counters' offsets and the running largest complex of this slab's
@@ -1603,10 +1766,124 @@ int kmc_dd_jumpers(kmc_sim* s, double S, int32_t cap, int32_t* ids, double* xs, 
   HIPCHK(s, hipStreamSynchronize(s->stream));
   const int32_t m = (int32_t)std::min<uint32_t>(cnt, (uint32_t)cap);
   if (m > 0) {
-    HIPCHK(s, hipMemcpy(ids, s->dd_ids, sizeof(int32_t) * m, hipMemcpyDeviceToHost));
-    HIPCHK(s, hipMemcpy(xs, s->dd_beads, sizeof(double) * m, hipMemcpyDeviceToHost));
+    HIPCHK(s, hipMemcpyAsync(ids, s->dd_ids, sizeof(int32_t) * m, hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(s, hipMemcpyAsync(xs, s->dd_beads, sizeof(double) * m, hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(s, hipStreamSynchronize(s->stream));
   }
   *n = (int32_t)cnt;  // may exceed cap: the caller asks again with room for all
+  return KMC_OK;
+}
+
+// ---- the device-resident exchange
+static bool dd_ready(kmc_sim* s) { return s && s->have_state && s->K.dd && s->dd_rep; }
+
+int kmc_dd_plan(kmc_sim* s, int32_t n_send, const int32_t* send_ids, int32_t n_recv, const int32_t* recv_ids,
+                const uint8_t* own, const uint8_t* band) {
+  if (!s || n_send < 0 || n_recv < 0 || !own || !band || (n_send > 0 && !send_ids) || (n_recv > 0 && !recv_ids))
+    return KMC_ERR_ARG;
+  if (!dd_ready(s)) return fail(s, KMC_ERR_ARG, "dd: no decomposed state");
+  const int N = s->K.N;
+  for (int i = 0; i < N; ++i)
+    if (own[i] > 1 || band[i] > 1 || (own[i] && band[i])) return fail(s, KMC_ERR_ARG, "dd: own / band flags");
+  for (int32_t i = 0; i < n_send; ++i)
+    if (send_ids[i] < 0 || send_ids[i] >= N || !own[send_ids[i]])
+      return fail(s, KMC_ERR_ARG, "dd: a sent protein out of range or not owned");
+  for (int32_t i = 0; i < n_recv; ++i)
+    if (recv_ids[i] < 0 || recv_ids[i] >= N || own[recv_ids[i]])
+      return fail(s, KMC_ERR_ARG, "dd: a received protein out of range or owned");
+  if (n_send > s->dd_send_cap) {
+    dfree(s, s->dd_send_ids);
+    dfree(s, s->dd_sendbuf);
+    s->dd_send_cap = std::max<int32_t>(n_send + n_send / 4, 1024);
+    int rc = dalloc(s, &s->dd_send_ids, (size_t)s->dd_send_cap);
+    rc |= dalloc(s, &s->dd_sendbuf, (size_t)s->dd_send_cap * KMC_DD_ROW);
+    if (rc != KMC_OK) return fail(s, KMC_ERR_HIP, "dd: send buffers");
+  }
+  if (n_recv > s->dd_recv_cap) {
+    dfree(s, s->dd_recv_ids);
+    s->dd_recv_cap = std::max<int32_t>(n_recv + n_recv / 4, 1024);
+    if (dalloc(s, &s->dd_recv_ids, (size_t)s->dd_recv_cap) != KMC_OK) return fail(s, KMC_ERR_HIP, "dd: receive ids");
+  }
+  if (n_send) HIPCHK(s, hipMemcpyAsync(s->dd_send_ids, send_ids, sizeof(int32_t) * n_send, hipMemcpyHostToDevice, s->stream));
+  if (n_recv) HIPCHK(s, hipMemcpyAsync(s->dd_recv_ids, recv_ids, sizeof(int32_t) * n_recv, hipMemcpyHostToDevice, s->stream));
+  HIPCHK(s, hipMemcpyAsync(s->dd_own, own, (size_t)N, hipMemcpyHostToDevice, s->stream));
+  HIPCHK(s, hipMemcpyAsync(s->dd_band, band, (size_t)N, hipMemcpyHostToDevice, s->stream));
+  HIPCHK(s, hipStreamSynchronize(s->stream));
+  s->dd_n_send = n_send;
+  s->dd_n_recv = n_recv;
+  return KMC_OK;
+}
+
+void* kmc_dd_send_buffer(kmc_sim* s) { return s ? (void*)s->dd_sendbuf : nullptr; }
+
+int kmc_dd_pack(kmc_sim* s, void* dst) {
+  if (!dd_ready(s)) return s ? fail(s, KMC_ERR_ARG, "dd: no decomposed state") : KMC_ERR_ARG;
+  unsigned char* out = dst ? (unsigned char*)dst : s->dd_sendbuf;
+  const int32_t n = s->dd_n_send;
+  if (n > 0) {
+    k_dd_pack<<<(unsigned)(((size_t)n * 56 + 255) / 256), 256, 0, s->stream>>>(s->K, s->d, n, s->dd_send_ids, out);
+    HIPCHK(s, hipGetLastError());
+  }
+  HIPCHK(s, hipStreamSynchronize(s->stream));
+  return KMC_OK;
+}
+
+int kmc_dd_unpack(kmc_sim* s, const void* src, int32_t first, int32_t n) {
+  if (!dd_ready(s)) return s ? fail(s, KMC_ERR_ARG, "dd: no decomposed state") : KMC_ERR_ARG;
+  if (first < 0 || n < 0 || (int64_t)first + n > s->dd_n_recv || (n > 0 && !src))
+    return fail(s, KMC_ERR_ARG, "dd: unpack range outside the receive plan");
+  if (n == 0) return KMC_OK;
+  k_dd_unpack<<<(unsigned)((n + 3) / 4), 256, 0, s->stream>>>(s->K, s->d, n, s->dd_recv_ids + first,
+                                                              (const unsigned char*)src, s->dd_band, s->dd_cut);
+  HIPCHK(s, hipGetLastError());
+  return KMC_OK;
+}
+
+int kmc_dd_finish(kmc_sim* s, double S, kmc_dd_report* out) {
+  static_assert(sizeof(DDRep) == sizeof(kmc_dd_report), "kmc_dd_report layout");
+  if (!out) return KMC_ERR_ARG;
+  if (!dd_ready(s)) return s ? fail(s, KMC_ERR_ARG, "dd: no decomposed state") : KMC_ERR_ARG;
+  k_dd_jumpers_rep<<<(s->K.N + 255) / 256, 256, 0, s->stream>>>(s->K, s->d, S);
+  HIPCHK(s, hipGetLastError());
+  uint32_t xc[2];
+  HIPCHK(s, hipMemcpyAsync(out, s->dd_rep, sizeof(DDRep), hipMemcpyDeviceToHost, s->stream));
+  HIPCHK(s, hipMemcpyAsync(xc, &s->d.ctl->dd_xcol, sizeof xc, hipMemcpyDeviceToHost, s->stream));
+  // the step's counts and lists start again at zero (the entries are
+  // overwritten before they are read)
+  HIPCHK(s, hipMemsetAsync(s->dd_rep, 0, offsetof(DDRep, jump_id), s->stream));
+  HIPCHK(s, hipStreamSynchronize(s->stream));
+  static_assert(offsetof(Ctl, dd_xbond) == offsetof(Ctl, dd_xcol) + sizeof(uint32_t), "Ctl dd counters");
+  out->xcol = xc[0];
+  out->xbond = xc[1];
+  // a halo protein's bonds changed under the kept complexes: register them anew
+  if (out->links) s->need_full = true;
+  s->clusters_valid = false;
+  return KMC_OK;
+}
+
+int kmc_dd_cut_count(kmc_sim* s, int32_t n, const int32_t* ids, int32_t* count) {
+  if (!count || n < 0 || (n > 0 && !ids)) return KMC_ERR_ARG;
+  if (!dd_ready(s)) return s ? fail(s, KMC_ERR_ARG, "dd: no decomposed state") : KMC_ERR_ARG;
+  const int N = s->K.N;
+  for (int32_t i = 0; i < n; ++i)
+    if (ids[i] < 0 || ids[i] >= N) return fail(s, KMC_ERR_ARG, "dd: index out of range");
+  std::vector<uint8_t> cut((size_t)N);
+  HIPCHK(s, hipMemcpyAsync(cut.data(), s->dd_cut, (size_t)N, hipMemcpyDeviceToHost, s->stream));
+  HIPCHK(s, hipStreamSynchronize(s->stream));
+  int32_t c = 0;
+  for (int32_t i = 0; i < n; ++i) c += cut[ids[i]] != 0;
+  *count = c;
+  return KMC_OK;
+}
+
+int kmc_list_growth(const kmc_sim* s) { return s ? s->grow : KMC_ERR_ARG; }
+
+int kmc_set_list_growth(kmc_sim* s, int32_t level) {
+  if (!s || level < -16 || level > 6) return KMC_ERR_ARG;
+  if (level == s->grow) return KMC_OK;
+  HIPCHK(s, hipStreamSynchronize(s->stream));
+  s->grow = level;
+  if (alloc_lists(s) != KMC_OK) return fail(s, KMC_ERR_HIP, "resizing the output lists failed");
   return KMC_OK;
 }
 

@@ -507,6 +507,30 @@ int load_state(const kmc_params* p, const char* path, kmc_state_view* v, std::st
   return validate(p, v, err);
 }
 
+// The window of a decomposed trajectory (kmc_dd_set_state): its local
+// numbering is monotone in the global one (receptors, then ligands: every
+// order the step takes — unit keys, BFS roots, the greedy reactions — is then
+// the global order restricted to the window), a global index fits an
+// exchanged link (global index + 1 in an int32), and ownership is 0 or 1.
+int dd_check(int32_t n, const int32_t* gid, const uint8_t* own, std::string* err) {
+  if (n < 0 || (n > 0 && (!gid || !own))) return KMC_ERR_ARG;
+  for (int32_t i = 0; i < n; ++i) {
+    if (gid[i] < 0 || gid[i] >= INT32_MAX) {
+      if (err) *err = "dd: global index out of range";
+      return KMC_ERR_ARG;
+    }
+    if (i > 0 && gid[i] <= gid[i - 1]) {
+      if (err) *err = "dd: global indices not increasing";
+      return KMC_ERR_ARG;
+    }
+    if (own[i] > 1) {
+      if (err) *err = "dd: ownership flag not 0 or 1";
+      return KMC_ERR_ARG;
+    }
+  }
+  return KMC_OK;
+}
+
 }  // namespace kmch_host
 
 // ------------------------------------------------------------------ C ABI (host-only part)
@@ -639,6 +663,9 @@ int kmc_host_load_state(const kmc_params* p, const char* path, kmc_state_view* v
   return kmch_host::load_state(p, path, v, &g_host_err);
 }
 int kmc_host_validate(const kmc_params* p, const kmc_state_view* v) { return kmch_host::validate(p, v, &g_host_err); }
+int kmc_host_dd_check(int32_t n, const int32_t* gid, const uint8_t* own) {
+  return kmch_host::dd_check(n, gid, own, &g_host_err);
+}
 
 int kmc_host_math(int op, const double* x, const double* y, double* out, int64_t n) {
   for (int64_t i = 0; i < n; ++i) {

@@ -113,6 +113,8 @@ struct Dev {
   const int32_t* gid;
   const uint8_t* dd_own;
   const double* dd_x0;
+  DDRep* dd_rep;  // the window's per-step exchange report (kmc_dd_finish): cross-slab bonds, jumpers, checks
+  uint32_t nkeys;  // unit keys (local reference indices) are < nkeys = N: a key outside latches ERR_RESOLVE
 };
 
 // one record (32 B): float reference point, ids, cis site
@@ -148,15 +150,20 @@ struct kmc_obs_dev {  // == kmc_obs
 #define B_ST(d, b, j) (d).b_int[(size_t)((j)-1) * NB + (b)]
 #define B_NEI(d, b, j) (d).b_int[(size_t)(4 + (j)-1) * NB + (b)]
 
+// a unit key outside [0, N): a protein no unit claimed (inconsistent bond
+// graph) or a corrupt record — latched as an error, never used as an index
+__device__ __forceinline__ bool bad_key(const Dev& d, int key) {
+  if ((uint32_t)key < d.nkeys) return false;
+  atomicOr(&d.ctl->err, ERR_RESOLVE);
+  return true;
+}
 __device__ __forceinline__ uint32_t state_of(const Dev& d, int key, uint32_t step) {
-  if (key < 0) {  // a protein no unit claimed: inconsistent bond graph
-    atomicOr(&d.ctl->err, ERR_RESOLVE);
-    return S_REJ;
-  }
+  if (bad_key(d, key)) return S_REJ;
   uint32_t v = ld_state(&d.ustate[key]);
   return (v >> 2) == (step & 0x3fffffffu) ? (v & 3u) : S_ACC;  // untouched this step: accepted
 }
 __device__ __forceinline__ void set_state(const Dev& d, int key, uint32_t step, uint32_t s) {
+  if (bad_key(d, key)) return;
   st_state(&d.ustate[key], ((step & 0x3fffffffu) << 2) | s);
 }
 
@@ -170,6 +177,18 @@ __device__ __forceinline__ uint32_t rkey(const KParams& P, const Dev& d, int r) 
 // protein of local reference index r is owned by this slab (always, outside
 // a decomposed trajectory)
 __device__ __forceinline__ bool dd_owned(const KParams& P, const Dev& d, int r) { return !P.dd || d.dd_own[r]; }
+// a bond formed between local proteins a and b (reference indices): one this
+// slab owns and one it holds as a halo copy joins units of two slabs — counted
+// and listed for the driver, which moves the joined unit to one owner
+__device__ __forceinline__ void dd_xbond(const Dev& d, int a, int b) {
+  if (d.dd_own[a] == d.dd_own[b]) return;
+  atomicAdd(&d.ctl->dd_xbond, 1u);
+  const uint32_t k = atomicAdd((uint32_t*)&d.dd_rep->n_xb, 1u);
+  if (k < DD_XCAP) {
+    d.dd_rep->xb[k][0] = a;
+    d.dd_rep->xb[k][1] = b;
+  }
+}
 
 __device__ __forceinline__ int cell_x(const KParams& P, double x) {
   int c = (int)__builtin_floor((x - P.gx0) / P.cs);
@@ -3346,6 +3365,7 @@ __device__ __forceinline__ bool rxn_pair(int2 me, float4 mp, float2 ms, int2 id,
 // ---------------------------------------------------------------- 4b. exact
 // u rejected; the first to reject it lists it for the commit
 __device__ __forceinline__ void mark_rej(const Dev& d, int u, uint32_t tag) {
+  if (bad_key(d, u)) return;
   uint32_t old = atomicMax(&d.ustate[u], tag | S_REJ);
   if (old != (tag | S_REJ)) sl_push(d.rej, make_int2(u, 0), &d.ctl->err);  // at most once per unit
 }
@@ -3435,6 +3455,7 @@ __device__ __forceinline__ void col_exact_one(const KParams& P, const Dev& d, co
     if (hit) atomicAdd(&d.ctl->cand_kind[2 * kk + 1], 1u);
   }
   if (!hit) return;
+  if (bad_key(d, u) || bad_key(d, kq)) return;
   if (P.dd && d.dd_own[u] != d.dd_own[kq]) atomicAdd(&d.ctl->dd_xcol, 1u);  // an owned unit against a halo unit
   if (kq >= u) {
     mark_rej(d, u, tag);
@@ -4184,8 +4205,7 @@ __device__ void rl_match(const KParams& P, const Dev& d) {
   auto apply = [&](uint64_t key) {
     int i = d.slot_of[(int)(key >> 34)], q = d.slot_of[(int)((key >> 2) & 0xffffffffu)], k = (int)(key & 3) + 2;
     int lb = q - NA;
-    if (P.dd && d.dd_own[(int)(key >> 34)] != d.dd_own[(int)((key >> 2) & 0xffffffffu)])
-      atomicAdd(&d.ctl->dd_xbond, 1u);  // a bond between an owned and a halo protein: the slabs re-partition
+    if (P.dd) dd_xbond(d, (int)(key >> 34), (int)((key >> 2) & 0xffffffffu));
     A_ST2(d, i) = 1;
     B_ST(d, lb, k) = 1;
     B_NEI(d, lb, k) = i + 1;
@@ -4234,8 +4254,7 @@ __device__ void cis_match(const KParams& P, const Dev& d) {
     uint32_t n = m;
     auto apply = [&](uint64_t key) {
       int i = d.slot_of[(int)(key >> 34)], q = d.slot_of[(int)((key >> 2) & 0xffffffffu)];
-      if (P.dd && d.dd_own[(int)(key >> 34)] != d.dd_own[(int)((key >> 2) & 0xffffffffu)])
-        atomicAdd(&d.ctl->dd_xbond, 1u);
+      if (P.dd) dd_xbond(d, (int)(key >> 34), (int)((key >> 2) & 0xffffffffu));
       A_ST3(d, i) = 1;
       A_ST3(d, q) = 1;
       A_NEI3(d, q) = i + 1;

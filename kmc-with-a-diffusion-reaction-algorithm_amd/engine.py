@@ -67,6 +67,7 @@ def load_library(path: Optional[str] = None):
     L.kmc_host_write_cpt.argtypes = [P(capi.Params), P(capi.StateView), C.c_char_p]
     L.kmc_host_init_random.argtypes = [P(capi.Params), P(capi.StateView)]
     L.kmc_host_validate.argtypes = [P(capi.Params), P(capi.StateView)]
+    L.kmc_host_dd_check.argtypes = [C.c_int32, C.c_void_p, C.c_void_p]
     L.kmc_host_save_state.argtypes = [P(capi.Params), P(capi.StateView), C.c_char_p]
     L.kmc_host_load_state.argtypes = [P(capi.Params), C.c_char_p, P(capi.StateView)]
     L.kmc_save_state.argtypes = [C.c_void_p, C.c_char_p]
@@ -81,6 +82,15 @@ def load_library(path: Optional[str] = None):
     L.kmc_dd_drift.argtypes = [C.c_void_p, P(C.c_double)]
     L.kmc_dd_counters.argtypes = [C.c_void_p, C.c_void_p]
     L.kmc_dd_jumpers.argtypes = [C.c_void_p, C.c_double, C.c_int32, C.c_void_p, C.c_void_p, P(C.c_int32)]
+    L.kmc_dd_plan.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.kmc_dd_pack.argtypes = [C.c_void_p, C.c_void_p]
+    L.kmc_dd_send_buffer.restype = C.c_void_p
+    L.kmc_dd_send_buffer.argtypes = [C.c_void_p]
+    L.kmc_dd_unpack.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32]
+    L.kmc_dd_finish.argtypes = [C.c_void_p, C.c_double, P(capi.DDReport)]
+    L.kmc_dd_cut_count.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, P(C.c_int32)]
+    L.kmc_list_growth.argtypes = [C.c_void_p]
+    L.kmc_set_list_growth.argtypes = [C.c_void_p, C.c_int32]
     for f in ("kmc_host_math", "kmc_device_math"):
         getattr(L, f).argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]
     _lib = L
@@ -137,6 +147,15 @@ def host_validate(params: capi.Params, hs: capi.HostState) -> int:
     return int(load_library().kmc_host_validate(C.byref(params), C.byref(v)))
 
 
+def host_dd_check(gid: np.ndarray, own: np.ndarray) -> int:
+    """kmc_dd_set_state's argument check on the host: 0 or KMC_ERR_ARG."""
+    gid = np.ascontiguousarray(gid, dtype=np.int32)
+    own = np.ascontiguousarray(own, dtype=np.uint8)
+    if gid.size != own.size:
+        raise ValueError("gid / own of one window")
+    return int(load_library().kmc_host_dd_check(gid.size, gid.ctypes.data, own.ctypes.data))
+
+
 def state_hash(params: capi.Params, hs: capi.HostState) -> int:
     v = hs.view()
     return int(load_library().kmc_state_hash(C.byref(params), C.byref(v)))
@@ -190,6 +209,7 @@ class Simulation:
 
     def __init__(self, params: capi.Params, device: int = 0):
         self.params = params
+        self.device = device  # HIP ordinal: the decomposed mode's exchange buffers live there
         L = load_library()
         h = C.c_void_p()
         rc = L.kmc_create(C.byref(params), device, C.byref(h))
@@ -318,6 +338,46 @@ class Simulation:
             if n.value <= cap:
                 return ids[: n.value], xs[: n.value]
             cap = n.value
+
+    # the device-resident exchange (kmc_dd_plan / pack / unpack / finish)
+    def dd_plan(self, send_ids: np.ndarray, recv_ids: np.ndarray, own: np.ndarray, band: np.ndarray) -> None:
+        send_ids = np.ascontiguousarray(send_ids, dtype=np.int32)
+        recv_ids = np.ascontiguousarray(recv_ids, dtype=np.int32)
+        own = np.ascontiguousarray(own, dtype=np.uint8)
+        band = np.ascontiguousarray(band, dtype=np.uint8)
+        n = self.params.n_a + self.params.n_b
+        if own.size != n or band.size != n:
+            raise ValueError("dd_plan: own / band sized n_a + n_b")
+        self._check(load_library().kmc_dd_plan(self._h, send_ids.size, send_ids.ctypes.data, recv_ids.size,
+                                               recv_ids.ctypes.data, own.ctypes.data, band.ctypes.data))
+
+    def dd_pack(self, dst: int = 0) -> int:
+        """Pack the plan's rows into device address dst (0: the handle's own
+        send buffer); returns the address written."""
+        L = load_library()
+        self._check(L.kmc_dd_pack(self._h, dst or None))
+        return dst or int(L.kmc_dd_send_buffer(self._h) or 0)
+
+    def dd_unpack(self, src: int, first: int, n: int) -> None:
+        self._check(load_library().kmc_dd_unpack(self._h, src, first, n))
+
+    def dd_finish(self, S: float) -> capi.DDReport:
+        rep = capi.DDReport()
+        self._check(load_library().kmc_dd_finish(self._h, S, C.byref(rep)))
+        return rep
+
+    def dd_cut_count(self, ids: np.ndarray) -> int:
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        c = C.c_int32()
+        self._check(load_library().kmc_dd_cut_count(self._h, ids.size, ids.ctypes.data, C.byref(c)))
+        return int(c.value)
+
+    @property
+    def list_growth(self) -> int:
+        return int(load_library().kmc_list_growth(self._h))
+
+    def set_list_growth(self, level: int) -> None:
+        self._check(load_library().kmc_set_list_growth(self._h, level))
 
     def set_timing(self, kernels=(), every: int = 1):
         """Bracket the named kernels with HIP events (empty: off), in every

@@ -1,4 +1,4 @@
-"""One KMC trajectory split over G slabs (SURVEY.md §8(f).4, DESIGN.md §8).
+"""One KMC trajectory split over G slabs (SURVEY.md §8(f).4, DESIGN.md §8a).
 
 The reference's step is one sequential loop over every unit
 (main.cpp:577-1872, Gauss–Seidel reads of R_new at 640-664 / 1762-1828)
@@ -7,45 +7,59 @@ global, yet a unit's outcome depends only on the units near it.  Here the box
 is cut into G slabs along x; each slab is simulated by its own engine handle
 (libkmc's kmc_dd_* entry points, include/kmc.h) over a *window*: the units it
 owns plus halo copies of every protein within `halo` Å (periodic in x) of
-them.  Because every random number is keyed by (seed, replica; step, global
-index, site) — never by who draws it — a handle computes exactly the
-trajectory's values for every protein whose neighbourhood it holds.
+them, and `margin` Å more.  Because every random number is keyed by (seed,
+replica; step, global index, site) — never by who draws it — a handle
+computes exactly the trajectory's values for every protein whose
+neighbourhood it holds.
 
 Per step, on every rank:
   1. step the window (kmc_step, one step): owned units and halo copies alike;
-  2. export the end-of-step state of the owned proteins other windows hold,
-     exchange (all-to-all), import the owners' state over the halo copies;
-  3. VERIFY: every halo protein close enough to interact with an owned one
-     (the *band*, within `halo / 2`) must have come out bit-identical to its
-     owner's result.  By induction over the step's decision order (unit keys,
-     then reaction edges) an owned protein can only be wrong if some band
-     protein's decision was, and that shows as a difference here; the outer
-     half of the halo only feeds the band's own computation;
-  4. all-reduce the observable shares (bond counts of owned receptors, owned
-     complexes; the largest complex by max) into the bond.dat record.
+  2. the halo exchange, on device memory: every window packs the end-of-step
+     rows of its owned proteins other windows hold (kmc_dd_pack, links as
+     global indices), the rows travel (G handles on one device: each window
+     reads its neighbours' send buffers directly; one rank per GPU: one
+     all_to_all_single of device buffers over RCCL), and every window unpacks
+     its owners' rows over its halo copies (kmc_dd_unpack: links found by a
+     binary search of the window's global indices, cut where they leave it);
+  3. VERIFY, counted on the device (kmc_dd_finish): every halo protein close
+     enough to interact with an owned one (the *band*, within `halo / 2`)
+     must have come out bit-identical to its owner's result, and none of its
+     links may leave the window.  By induction over the step's decision order
+     (unit keys, then reaction edges) an owned protein can only be wrong if
+     some band protein's decision was, and that shows as a difference here;
+     the outer half of the halo only feeds the band's own computation;
+  4. all-gather the observable shares (bond counts of owned receptors, owned
+     complexes; the largest complex by max) into the bond.dat record, with
+     each rank's check results.
 Presence.  With band B = halo / 2 and S = (B − R_INT) / 2, a protein that
-stays within S (in x) of where it was at the last partition meets, within
-R_INT, only proteins its owner's window holds in the band.  The few that
-move further (association snaps and lay-downs jump a receptor by up to
-≈ 180 Å) are *jumpers*, checked after every step against the partition:
-(J_B) a jumper stays within S of its own slab's proteins, (J_A) a jumper is
-at least R_INT + S from the proteins of every slab that does not hold it in
-its band.  Only accepted positions need checking: a unit whose proposal met
-a protein its window lacks can only have lost a collision, so a rejection is
-right and an acceptance puts the proposal under the checks.
+stays within S (in x) of where it was at the last partition (its *anchor*)
+meets, within R_INT, only proteins its owner's window holds in the band.  The
+few that move further (association snaps and lay-downs jump a receptor by up
+to ≈ 180 Å) are *jumpers*, listed by kmc_dd_finish: (J_B) a jumper stays
+within S of its own slab's anchors, (J_A) a jumper is at least R_INT + S from
+the anchors of every slab that does not hold it in its band.  Only accepted
+positions need checking: a unit whose proposal met a protein its window lacks
+can only have lost a collision, so a rejection is right and an acceptance
+puts the proposal under the checks.
+Cross-slab bonds.  A unit must be owned whole.  When a bond joins units of
+two slabs (kmc_dd_finish lists it), the joined unit moves to the owner of its
+lowest-index member: the windows are kept, only ownership, band and the
+exchange lists change (kmc_dd_plan), provided the new owner holds every
+protein within `halo` of the moved anchors (C1) and every new band protein's
+unit whole (C2, kmc_dd_cut_count); otherwise the trajectory re-partitions.
 Re-partition (a collective *rebuild* from the assembled global state, which
-is also the rollback checkpoint) happens when a bond joined units of two
-slabs (a unit must be owned whole) and when jumpers accumulate; a failed
-verification or jumper check rolls back to the checkpoint, replays to the
-step before, re-partitions there and retries (a second failure widens the
-halo): the run is exact whenever it completes.
+is also the rollback checkpoint) also happens when jumpers accumulate; a
+failed verification or jumper check rolls back to the checkpoint, replays to
+the step before, re-partitions there and retries (a second failure widens
+the halo): the run is exact whenever it completes.
 
 This module is the host side of the decomposed path; the engine under each
 rank is anything with the kmc_dd_* contract (engine.Simulation on a gfx950
-device; the tests also run the same driver over the CPU oracle).  The
-exchange goes through a Comm: LocalComm (G ranks as threads of one process,
-e.g. G windows on one GPU) or TorchComm (one rank per process over
-torch.distributed).
+device; the tests also run the same driver over the CPU oracle, whose
+"device" addresses are host addresses).  The exchange goes through a Comm:
+LocalComm (G ranks as threads of one process, e.g. G windows on one GPU) or
+TorchComm (one rank per process over torch.distributed: device buffers over
+RCCL, host staging over gloo).
 """
 from __future__ import annotations
 
@@ -64,8 +78,13 @@ from . import capi
 # < 60 Å apart, each within 35 Å of its ligand's [1][1] (DESIGN.md §cell
 # list) — 130 Å; R–L gates are shorter (< 104 Å), receptor pairs < 56 Å.
 R_INT = 140.0
-# re-partition when more than this many jumpers (all slabs) have accumulated
-JUMPERS_MAX = 64
+# re-partition when more jumpers than the exchange report lists (all slabs)
+# have accumulated
+JUMPERS_MAX = capi.DD_JCAP
+# a step that fails its checks this many times in a row (each retry from a
+# wider partition) is not recoverable
+MAX_TRIES = 8
+ROW = capi.DD_ROW
 
 A_LINKS = (2, 4)  # kmc_state_view a_int rows holding protein links (nei2, nei3)
 B_LINKS = (4, 5, 6, 7)
@@ -75,9 +94,16 @@ class SlabError(RuntimeError):
     pass
 
 
+def _engine_error(e: BaseException) -> Optional[int]:
+    """The KMC_ERR_* code of an engine (libkmc or oracle) error, else None."""
+    return getattr(e, "code", None)
+
+
 # ---------------------------------------------------------------- comms
 class LocalComm:
-    """G ranks as threads of one process (one engine handle each)."""
+    """G ranks as threads of one process (one engine handle each).  The halo
+    exchange reads the neighbours' send buffers in place: G handles on one
+    device (or the oracle's host buffers)."""
 
     def __init__(self, world: int):
         self.world = world
@@ -91,57 +117,75 @@ class LocalComm:
         self._bar.wait()
         return out
 
-    def alltoall(self, rank: int, objs: list) -> list:
-        allv = self.allgather(rank, objs)
-        return [allv[src][rank] for src in range(self.world)]
+    def exchange(self, rank: int, me: "SlabRank") -> None:
+        ptr = me.eng.dd_pack() if me.eng_ok else None
+        peers = self.allgather(rank, (ptr, me.send_first))
+        if not me.eng_ok:
+            return
+        for src in range(self.world):
+            n = me.recv_n[src]
+            if src == rank or n == 0:
+                continue
+            sptr, sfirst = peers[src]
+            if sptr is None:  # the source's step failed: the step is redone anyway
+                continue
+            me.eng.dd_unpack(sptr + sfirst[rank] * ROW, me.recv_first[src], n)
 
 
 class TorchComm:
-    """One rank per process over an initialised torch.distributed group."""
+    """One rank per process over an initialised torch.distributed group.  The
+    halo rows go through one all_to_all_single per step: on device buffers
+    when the backend is a device one (nccl = RCCL on ROCm, one GPU per rank),
+    through host memory over gloo."""
 
     def __init__(self):
         import torch.distributed as dist
 
         self.dist = dist
         self.world = dist.get_world_size()
+        self.device_backend = dist.get_backend() != "gloo"
+        self._bufs = {}
 
     def allgather(self, rank: int, obj):
         out = [None] * self.world
         self.dist.all_gather_object(out, obj)
         return out
 
-    def alltoall(self, rank: int, objs: list) -> list:
-        """objs[r] to rank r; returns the messages from every rank.  Over gloo
-        each message goes only to its destination (sizes all-gathered, then
-        point-to-point); other backends all-gather every message."""
-        if self.dist.get_backend() != "gloo":
-            allv = self.allgather(rank, objs)
-            return [allv[src][rank] for src in range(self.world)]
-        import pickle
-
+    def _buf(self, key, nbytes, device):
         import torch
 
-        W = self.world
-        data = [b"" if r == rank or objs[r] is None else pickle.dumps(objs[r], protocol=5) for r in range(W)]
-        sizes = [torch.zeros(W, dtype=torch.int64) for _ in range(W)]
-        self.dist.all_gather(sizes, torch.tensor([len(x) for x in data], dtype=torch.int64))
-        reqs, bufs = [], {}
-        for r in range(W):
-            if r == rank:
-                continue
-            if data[r]:
-                reqs.append(self.dist.isend(torch.frombuffer(bytearray(data[r]), dtype=torch.uint8), r))
-            n = int(sizes[r][rank])
-            if n:
-                bufs[r] = torch.empty(n, dtype=torch.uint8)
-                reqs.append(self.dist.irecv(bufs[r], r))
-        for q in reqs:
-            q.wait()
-        out = [None] * W
-        out[rank] = objs[rank]
-        for r, b in bufs.items():
-            out[r] = pickle.loads(b.numpy().tobytes())  # (a peer rank's own message)
-        return out
+        b = self._bufs.get(key)
+        if b is None or b.numel() < nbytes or b.device != device:
+            b = torch.empty(max(nbytes, ROW), dtype=torch.uint8, device=device)
+            self._bufs[key] = b
+        return b
+
+    def exchange(self, rank: int, me: "SlabRank") -> None:
+        import torch
+
+        dev = getattr(me.eng, "device", None)
+        if self.device_backend and dev is None:
+            raise SlabError("a device backend exchanges device buffers: the ranks' engines must be on GPUs")
+        edev = torch.device("cuda", dev) if dev is not None else torch.device("cpu")
+        wdev = edev if self.device_backend else torch.device("cpu")  # where the collective's buffers live
+        ns, nr = me.n_send * ROW, me.n_recv * ROW
+        send = self._buf("send", ns, edev)
+        if me.eng_ok:
+            me.eng.dd_pack(send.data_ptr())
+        else:
+            send.zero_()
+        if wdev != edev:
+            send = send[:ns].to(wdev)
+        recv = self._buf("recv", nr, wdev)
+        self.dist.all_to_all_single(recv[:nr], send[:ns], [n * ROW for n in me.recv_n],
+                                    [n * ROW for n in me.send_n])
+        if wdev != edev:
+            recv = self._buf("recv_dev", nr, edev)
+            recv[:nr].copy_(self._bufs["recv"][:nr])
+        if edev.type == "cuda":
+            torch.cuda.synchronize(edev)
+        if me.eng_ok and me.n_recv:
+            me.eng.dd_unpack(recv.data_ptr(), 0, me.n_recv)
 
 
 def run_threads(world: int, fn: Callable[[int], object]) -> list:
@@ -166,8 +210,6 @@ def run_threads(world: int, fn: Callable[[int], object]) -> list:
     if err:
         real = [e for e in err if not isinstance(e, threading.BrokenBarrierError)]
         if len(real) > 1:
-            real[0].add_note("other ranks: " + "; ".join(repr(e) for e in real[1:])) if hasattr(real[0], "add_note") \
-                else None
             real[0].args = real[0].args + tuple(f"(also: {e!r})" for e in real[1:])
         raise (real or err)[0]
     return out
@@ -213,21 +255,30 @@ def units(hs: capi.HostState) -> np.ndarray:
         dst.append(v[k] - 1)
     src = np.concatenate(src).astype(np.int64)
     dst = np.concatenate(dst).astype(np.int64)
-    while True:  # min-label propagation to a fixed point (components are small)
-        m = np.minimum(lab[src], lab[dst])
-        new = lab.copy()
-        np.minimum.at(new, src, m)
-        np.minimum.at(new, dst, m)
-        new = new[new]
-        if np.array_equal(new, lab):
+    if src.size == 0:
+        return lab
+    # min-label propagation to a fixed point over the bonded proteins only
+    # (components are small; most proteins are free)
+    nodes = np.unique(np.concatenate([src, dst]))
+    s = np.searchsorted(nodes, src)
+    t = np.searchsorted(nodes, dst)
+    sub = nodes.copy()
+    while True:
+        m = np.minimum(sub[s], sub[t])
+        new = sub.copy()
+        np.minimum.at(new, s, m)
+        np.minimum.at(new, t, m)
+        new = new[np.searchsorted(nodes, new)]
+        if np.array_equal(new, sub):
+            lab[nodes] = sub
             return lab
-        lab = new
+        sub = new
 
 
 def periodic_dist(x: np.ndarray, ref_sorted: np.ndarray, L: float) -> np.ndarray:
     """Distance (periodic in L) of each x to the nearest value of ref_sorted."""
     if ref_sorted.size == 0:
-        return np.full(x.shape, np.inf)
+        return np.full(np.shape(x), np.inf)
     j = np.searchsorted(ref_sorted, x)
     lo = ref_sorted[(j - 1) % ref_sorted.size]
     hi = ref_sorted[j % ref_sorted.size]
@@ -238,14 +289,18 @@ def periodic_dist(x: np.ndarray, ref_sorted: np.ndarray, L: float) -> np.ndarray
     return np.minimum(d1, d2)
 
 
+def wrap(x, L: float):
+    """x wrapped into [-L/2, L/2)."""
+    return x - L * np.floor((x + L / 2) / L)
+
+
 @dataclass
 class Window:
     gids: np.ndarray          # global indices held, increasing (receptors first)
     own: np.ndarray           # uint8 per held protein
-    band: np.ndarray          # bool per held protein: halo within halo / 2 of an owned protein
+    band: np.ndarray          # bool per held protein: halo within halo / 2 of an owned anchor
     n_a: int = 0
     n_b: int = 0
-    loc: dict = field(default_factory=dict)  # global index -> local index
 
 
 @dataclass
@@ -255,37 +310,56 @@ class Plan:
     owner: np.ndarray         # rank per global protein
     windows: List[Window]
     halo: float
-    own_x: List[np.ndarray]   # per rank: sorted wrapped x of its owned proteins
+    xw: np.ndarray            # anchors: wrapped x of every protein at the partition
+    xs: np.ndarray            # the anchors sorted
+    xs_order: np.ndarray      # ... and their global indices
+    held: List[np.ndarray]    # per rank: bool per global protein, held by its window
+    own_x: List[np.ndarray]   # per rank: sorted anchors of its owned proteins
     near: List[np.ndarray]    # per rank: bool per global protein, owned or in its band
+    L: float = 0.0
+
+    def within(self, x: float, h: float) -> np.ndarray:
+        """Global indices of the proteins whose anchor is within h of x (periodic)."""
+        L = self.L
+        lo, hi = x - h, x + h
+        spans = [(lo, hi)]
+        if lo < -L / 2:
+            spans = [(lo + L, L / 2), (-L / 2, hi)]
+        elif hi >= L / 2:
+            spans = [(lo, L / 2), (-L / 2, hi - L)]
+        idx = [self.xs_order[np.searchsorted(self.xs, a, "left"):np.searchsorted(self.xs, b, "right")]
+               for a, b in spans]
+        return np.concatenate(idx) if len(idx) > 1 else idx[0]
 
 
-def make_plan(p: capi.Params, hs: capi.HostState, G: int, halo: float) -> Plan:
+def make_plan(p: capi.Params, hs: capi.HostState, G: int, halo: float, margin: float = 0.0) -> Plan:
     L = p.box_x
     n_a = hs.n_a
-    x = ref_x(hs)
-    xw = x - L * np.floor((x + L / 2) / L)  # wrapped into [-L/2, L/2)
+    xw = wrap(ref_x(hs), L)
     lab = units(hs)
     slab = np.clip(np.floor((xw[lab] + L / 2) / (L / G)).astype(np.int64), 0, G - 1)  # by the unit's lead
     owner = slab
     band_w = halo / 2
-    windows, own_x, near = [], [], []
+    order = np.argsort(xw, kind="stable")
+    windows, own_x, near, held_all = [], [], [], []
     for r in range(G):
         own = owner == r
         ref = np.sort(xw[own])
         own_x.append(ref)
         d = periodic_dist(xw, ref, L)
-        held = own | (d < halo)
+        held = own | (d < halo + margin)
         band = ~own & (d < band_w)
         near.append(own | band)
         # a band protein's whole unit is held: its local computation then
         # sees every member (a unit is moved and decided as one)
         held |= np.isin(lab, np.unique(lab[band]))
+        held_all.append(held)
         gids = np.flatnonzero(held).astype(np.int32)
         w = Window(gids=gids, own=own[gids].astype(np.uint8), band=band[gids],
                    n_a=int((gids < n_a).sum()), n_b=int((gids >= n_a).sum()))
-        w.loc = {int(g): i for i, g in enumerate(gids)}
         windows.append(w)
-    return Plan(owner=owner, windows=windows, halo=halo, own_x=own_x, near=near)
+    return Plan(owner=owner, windows=windows, halo=halo, xw=xw, xs=xw[order], xs_order=order, held=held_all,
+                own_x=own_x, near=near, L=L)
 
 
 def window_state(hs: capi.HostState, w: Window) -> capi.HostState:
@@ -322,36 +396,60 @@ def window_state(hs: capi.HostState, w: Window) -> capi.HostState:
     return out
 
 
+def _components(nodes: np.ndarray, edges: np.ndarray) -> List[np.ndarray]:
+    """Connected components of a small graph (nodes sorted; edges [m, 2])."""
+    lab = np.arange(nodes.size)
+    if edges.size:
+        s = np.searchsorted(nodes, edges[:, 0])
+        t = np.searchsorted(nodes, edges[:, 1])
+        while True:
+            m = np.minimum(lab[s], lab[t])
+            new = lab.copy()
+            np.minimum.at(new, s, m)
+            np.minimum.at(new, t, m)
+            new = new[new]
+            if np.array_equal(new, lab):
+                break
+            lab = new
+    return [nodes[lab == v] for v in np.unique(lab)]
+
+
 # ---------------------------------------------------------------- one rank
 class SlabRank:
     """Rank `rank` of a G-slab trajectory.  make_engine(params) returns a fresh
     handle with the kmc_dd_* methods for a window's proteins."""
 
     def __init__(self, p: capi.Params, rank: int, comm, make_engine: Callable, halo: float = 900.0,
-                 gather_every: int = 0):
+                 gather_every: int = 0, margin: Optional[float] = None):
         self.p = p
         self.rank = rank
         self.comm = comm
         self.G = comm.world
         self.make_engine = make_engine
         self.halo = float(halo)
+        # the window holds `margin` Å beyond the halo, so that a unit joined
+        # across the cut can move to its new owner without a re-partition (C1)
+        self.margin = float(400.0 if margin is None else margin)
         self.gather_every = gather_every  # assemble the global state every k steps (tests: 1)
         self.eng = None
+        self.eng_ok = True
+        self.grow = 0  # output-list growth carried to the handles of a rebuild (kmc_list_growth)
         self.plan: Optional[Plan] = None
         self.win: Optional[Window] = None
         self.step_no = 0
         self.counters = np.zeros(5, dtype=np.int32)
         self.ckpt: Optional[capi.HostState] = None
         self.history: list = []  # global records since the checkpoint (replay check)
-        self.stats = dict(steps=0, rebuilds=0, rebuild_bond=0, rebuild_jumpers=0, rollbacks=0, replayed=0, xcol=0,
-                          xbond=0,
-                          exchanged=0, verified=0, jumpers=0, held=0, owned=0, why=[],
-                          sec=dict(step=0.0, export=0.0, comm=0.0, imp=0.0, jumpers=0.0, gather=0.0, rebuild=0.0))
+        self.stats = dict(steps=0, rebuilds=0, rebuild_bond=0, rebuild_jumpers=0, transfers=0, moved=0,
+                          rollbacks=0, replayed=0, xcol=0, xbond=0, exchanged=0, verified=0, jumpers=0, held=0,
+                          owned=0, why=[],
+                          sec=dict(step=0.0, exchange=0.0, finish=0.0, jumpers=0.0, gather=0.0, transfer=0.0,
+                                   rebuild=0.0))
         self.last_global: Optional[capi.HostState] = None
         self._xc = (0, 0)
         self._njump = 0  # jumpers after the last step, all slabs
         # debug (KMC_SLABS_CHECK=1): the window's bond graph and extent bounds
-        # validated (kmc_host_validate) after every import
+        # validated (kmc_host_validate) after every exchange
         self.check = os.environ.get("KMC_SLABS_CHECK") == "1"
 
     @property
@@ -380,7 +478,7 @@ class SlabRank:
         self.ckpt.counters[:] = self.counters
         self.ckpt.step = self.step_no
         self.history = []
-        self.plan = make_plan(self.p, hs, self.G, self.halo)
+        self.plan = make_plan(self.p, hs, self.G, self.halo, self.margin)
         w = self.plan.windows[self.rank]
         self.win = w
         ws = window_state(hs, w)
@@ -389,48 +487,62 @@ class SlabRank:
         ctl5 = [c[0] - (rl + mono + cis), c[1] - rl, c[2] - cis, c[3] - mono, c[4]] if self.rank == 0 else [0] * 5
         if self.eng is not None:
             self.eng.close()
+            self.eng = None
         q = capi.Params.from_buffer_copy(self.p)
         q.n_a, q.n_b = w.n_a, w.n_b
         self.q = q
         self.eng = self.make_engine(q)
+        if self.grow:
+            self.eng.set_list_growth(self.grow)
         self.eng.dd_set_state(ws, w.gids, w.own, ctl5)
+        self.eng_ok = True
         self._xc = (0, 0)
         self._njump = 0
-        # export lists: my owned proteins held by each other window (local
-        # indices here, global in transit)
-        self.exp = []
-        for r in range(self.G):
-            if r == self.rank:
-                self.exp.append(np.zeros(0, np.int32))
-                continue
-            g = np.intersect1d(w.gids[w.own == 1], self.plan.windows[r].gids, assume_unique=True)
-            self.exp.append(np.array([w.loc[int(x)] for x in g], dtype=np.int32))
-        self.g2l = np.zeros(self.p.n_a + self.p.n_b + 1, dtype=np.int32)  # global + 1 -> local + 1
-        self.g2l[w.gids + 1] = np.arange(1, w.gids.size + 1, dtype=np.int32)
-        self.stats["held"] = int(w.gids.size)
-        self.stats["owned"] = int(w.own.sum())
+        self._set_lists()
         self.stats["rebuilds"] += 1
 
-    def _links(self, ints: np.ndarray, local_ids: np.ndarray, to_global: bool, win: Window) -> np.ndarray:
-        """Translate the link fields of exchanged records (local <-> global + 1)."""
-        out = ints.copy()
-        rec = local_ids < win.n_a
-        for f in range(8):
-            col = out[:, f]
-            is_link = (rec & ((f == 2) | (f == 4))) | (~rec & (f >= 4))
-            m = is_link & (col > 0)
-            if to_global:
-                col[m] = win.gids[col[m] - 1] + 1
-            else:
-                col[m] = self.g2l[col[m]]
-        return out
+    def _set_lists(self) -> None:
+        """The window's exchange plan from the partition: it sends its owned
+        proteins each other window holds (to each in increasing global index)
+        and receives every protein it holds but does not own from its owner."""
+        w, plan, G = self.win, self.plan, self.G
+        own = w.own == 1
+        own_g = w.gids[own]
+        send, self.send_n = [], [0] * G
+        for dst in range(G):
+            if dst == self.rank:
+                continue
+            g = own_g[plan.held[dst][own_g]]
+            send.append(np.searchsorted(w.gids, g).astype(np.int32))
+            self.send_n[dst] = int(g.size)
+        src_of = plan.owner[w.gids]
+        recv, self.recv_n = [], [0] * G
+        for src in range(G):
+            if src == self.rank:
+                continue
+            loc = np.flatnonzero((src_of == src) & ~own).astype(np.int32)
+            recv.append(loc)
+            self.recv_n[src] = int(loc.size)
+        self.send_first = [int(x) for x in np.concatenate([[0], np.cumsum(self.send_n)[:-1]])]
+        self.recv_first = [int(x) for x in np.concatenate([[0], np.cumsum(self.recv_n)[:-1]])]
+        send_ids = np.concatenate(send) if send else np.zeros(0, np.int32)
+        recv_ids = np.concatenate(recv) if recv else np.zeros(0, np.int32)
+        self.n_send, self.n_recv = int(send_ids.size), int(recv_ids.size)
+        self.n_verify = int(w.band[recv_ids].sum())
+        self.eng.dd_plan(send_ids, recv_ids, w.own, w.band.astype(np.uint8))
+        self.stats["held"] = int(w.gids.size)
+        self.stats["owned"] = int(own.sum())
 
     def global_state(self) -> capi.HostState:
         """Collective: the trajectory's state assembled from every slab's owned proteins."""
         w = self.win
         ids = np.flatnonzero(w.own).astype(np.int32)
         beads, ints = self.eng.dd_export(ids)
-        ints = self._links(ints, ids, True, w)
+        rec = ids < w.n_a
+        for f in range(8):  # links local + 1 -> global + 1
+            col = ints[:, f]
+            m = ((rec & ((f == 2) | (f == 4))) | (~rec & (f >= 4))) & (col > 0)
+            col[m] = w.gids[col[m] - 1] + 1
         parts = self.comm.allgather(self.rank, (w.gids[ids], beads, ints))
         n_a, n_b = self.p.n_a, self.p.n_b
         hs = capi.HostState(n_a, n_b)
@@ -452,7 +564,12 @@ class SlabRank:
         tries = 0
         while rec is None:  # a check failed on some slab: back to the step before, re-partition, retry
             tries += 1
-            self._recover(widen=tries > 1)
+            if tries > MAX_TRIES or self.halo > 64 * self.p.box_x:
+                raise SlabError(f"step {self.step_no + 1} does not pass its checks after {tries - 1} retries "
+                                f"(halo {self.halo:.0f} Å): {self.stats['why'][-3:]}")
+            # a repeated failure, or one right after the partition (nothing to
+            # replay: the same partition would fail again), widens the halo
+            self._recover(widen=tries > 1 or not self.history)
             rec = self._one()
         self._remember(rec)
         self.stats["steps"] += 1
@@ -470,14 +587,12 @@ class SlabRank:
             self._rebuild_from(self.global_state())
         return self._step_exchange()
 
-    def _jumper_check(self) -> int:
+    def _jumper_check(self, ids: np.ndarray, xs: np.ndarray) -> int:
         """Jumpers of my slab violating J_A / J_B (module docstring): count."""
-        ids, xs = self.eng.dd_jumpers(self.S)
-        self._my_jumpers = int(ids.size)
         if ids.size == 0:
             return 0
         L = self.p.box_x
-        xw = xs - L * np.floor((xs + L / 2) / L)
+        xw = wrap(xs, L)
         g = self.win.gids[ids]
         bad = int((periodic_dist(xw, self.plan.own_x[self.rank], L) > self.S).sum())  # J_B
         for r in range(self.G):
@@ -488,76 +603,87 @@ class SlabRank:
                 bad += int((periodic_dist(xw[far], self.plan.own_x[r], L) < R_INT + self.S).sum())  # J_A
         return bad
 
-    def _step_exchange(self) -> Optional[np.ndarray]:
+    def _cross_units(self, rep) -> Optional[list]:
+        """The units joined by this step's cross-slab bonds, as sorted global
+        indices, from this window's links (None: more bonds than listed)."""
+        if rep.n_xb == 0:
+            return []
+        if rep.n_xb > capi.DD_XCAP:
+            return None
         w = self.win
+        pairs = rep.cross_bonds()
+        nodes = np.unique(pairs.ravel()).astype(np.int32)
+        edges = [pairs]
+        frontier = nodes
+        while frontier.size:
+            _, ints = self.eng.dd_export(frontier)
+            rec = frontier < w.n_a
+            nb = []
+            for f in range(8):
+                m = ((rec & ((f == 2) | (f == 4))) | (~rec & (f >= 4))) & (ints[:, f] > 0)
+                if m.any():
+                    e = np.stack([frontier[m], ints[m, f] - 1], axis=1)
+                    edges.append(e)
+                    nb.append(e[:, 1])
+            new = np.setdiff1d(np.concatenate(nb) if nb else np.zeros(0, np.int32), nodes).astype(np.int32)
+            nodes = np.union1d(nodes, new).astype(np.int32)
+            frontier = new
+        comps = _components(nodes, np.concatenate(edges).astype(np.int64))
+        return [w.gids[c].astype(np.int64) for c in comps]
+
+    def _step_exchange(self) -> Optional[np.ndarray]:
         sec = self.stats["sec"]  # host seconds by phase (tools/slab_rate.py)
         t0 = time.perf_counter()
-        part = self.eng.step(1)[0]
-        xcol, xbond = self.eng.dd_counters()
+        part, fail, err = None, False, None
+        try:
+            part = self.eng.step(1)[0].copy()
+        except Exception as e:  # noqa: BLE001 — every rank must learn of it (the shares below)
+            self.eng_ok = False
+            if _engine_error(e) == capi.ERR_CAPACITY:
+                fail = True  # the lists were full: redo the step from the checkpoint with larger ones
+                self.grow = max(self.grow, int(getattr(self.eng, "list_growth", 0)))
+            else:
+                err = f"rank {self.rank}: {e!r}"
         t1 = time.perf_counter()
         sec["step"] += t1 - t0
-        dcol, dbond = xcol - self._xc[0], xbond - self._xc[1]
-        self._xc = (xcol, xbond)
-        # halo exchange: my owned proteins' end state to every window holding them
-        out = []
-        for r in range(self.G):
-            ids = self.exp[r]
-            if ids.size == 0:
-                out.append(None)
-                continue
-            beads, ints = self.eng.dd_export(ids)
-            out.append((w.gids[ids], beads, self._links(ints, ids, True, w)))
+        # the halo exchange: my owned proteins' end state to every window holding them
+        self.comm.exchange(self.rank, self)
         t2 = time.perf_counter()
-        sec["export"] += t2 - t1
-        got = self.comm.alltoall(self.rank, out)
-        t3 = time.perf_counter()
-        sec["comm"] += t3 - t2
-        bad = 0
-        nver = 0
-        for src, msg in enumerate(got):
-            if msg is None:
-                continue
-            g, beads, ints = msg
-            loc = self.g2l[g + 1] - 1
-            if (loc < 0).any():
-                raise SlabError("a halo record of a protein this window does not hold")
-            li = self._links(ints, loc, False, w)
-            # a link to a protein outside the window (outer halo only): cut it
-            lost = (ints > 0) & (li == 0)
-            lost_any = lost.any(axis=1)
-            if lost_any.any():
-                if w.band[loc[lost_any]].any():
-                    bad += 1  # a band unit reached outside the window: re-partition
-                rec = loc < w.n_a
-                for k in np.flatnonzero(lost_any):
-                    for f in np.flatnonzero(lost[k]):
-                        if rec[k]:
-                            li[k, 0 if f == 2 else 1] = 0
-                            if f == 2:
-                                li[k, 3] = 0
-                        else:
-                            li[k, f - 4] = 0
-            flags = self.eng.dd_import(loc, beads, li)
-            vb = w.band[loc]
-            nver += int(vb.sum())
-            bad += int((flags[vb] != 0).sum())
-            self.stats["exchanged"] += int(loc.size)
-        self.stats["verified"] += nver
-        if self.check:
-            from . import engine as _engine
+        sec["exchange"] += t2 - t1
+        bad = jbad = nj = 0
+        dcol = dbond = 0
+        xunits: Optional[list] = []
+        if self.eng_ok:
+            rep = self.eng.dd_finish(self.S)
+            t3 = time.perf_counter()
+            sec["finish"] += t3 - t2
+            bad = rep.bad
+            dcol, dbond = rep.xcol - self._xc[0], rep.xbond - self._xc[1]
+            self._xc = (rep.xcol, rep.xbond)
+            self.stats["exchanged"] += self.n_recv
+            self.stats["verified"] += self.n_verify
+            nj = rep.n_jump
+            jbad = self._jumper_check(*rep.jumpers())
+            xunits = self._cross_units(rep)
+            if self.check:
+                from . import engine as _engine
 
-            rc = _engine.host_validate(self.q, self.eng.get_state())
-            if rc != 0:
-                raise SlabError(f"rank {self.rank}: window state invalid ({rc}) after the import of step "
-                                f"{self.step_no + 1}: {_engine.load_library().kmc_host_last_error().decode()}")
-        t4 = time.perf_counter()
-        sec["imp"] += t4 - t3
-        jbad = self._jumper_check()
+                rc = _engine.host_validate(self.q, self.eng.get_state())
+                if rc != 0:
+                    err = (f"rank {self.rank}: window state invalid ({rc}) after the exchange of step "
+                           f"{self.step_no + 1}: {_engine.load_library().kmc_host_last_error().decode()}")
+            sec["jumpers"] += time.perf_counter() - t3
         t5 = time.perf_counter()
-        sec["jumpers"] += t5 - t4
-        # the step's record from every slab's share; checks, triggers
-        shares = self.comm.allgather(self.rank, (part.copy(), bad, jbad, dbond, dcol, self._my_jumpers))
+        # the step's record from every slab's share, the checks and triggers:
+        # every rank decides alike
+        shares = self.comm.allgather(self.rank, (part, bad, jbad, dbond, dcol, nj, xunits, fail, err))
         sec["gather"] += time.perf_counter() - t5
+        errs = [s[8] for s in shares if s[8]]
+        if errs:
+            raise SlabError("; ".join(errs))
+        if any(s[7] for s in shares):
+            self.stats["why"].append((self.step_no + 1, "capacity", 0, 0))
+            return None
         if any(s[1] or s[2] for s in shares):
             self.stats["why"].append((self.step_no + 1, "verify" if any(s[1] for s in shares) else "jumper",
                                       sum(s[1] for s in shares), sum(s[2] for s in shares)))
@@ -571,21 +697,79 @@ class SlabRank:
         self.step_no = int(r0["step"])
         self.counters[:] = [r0["bond_num"], r0["bond_num_rl"], r0["bond_num_cis"], r0["bond_num_mono_cis"],
                             r0["protein_num_in_max_complex"]]
-        need = any(s[3] for s in shares)  # a bond between two slabs' units: one owner for the new unit
-        if need or (self.gather_every and self.step_no % self.gather_every == 0):
+        gs = None
+        if any(s[6] is None for s in shares):  # more cross-slab bonds than listed
             gs = self.global_state()
-            self.last_global = gs
-            if need:
-                self.stats["rebuild_bond"] += 1
-                self._rebuild_from(gs)
+            self.stats["rebuild_bond"] += 1
+            self._rebuild_from(gs)
+        else:
+            joined = [u for s in shares for u in s[6]]
+            if joined:
+                t6 = time.perf_counter()
+                ok = self._transfer(joined)
+                sec["transfer"] += time.perf_counter() - t6
+                if not ok:
+                    gs = self.global_state()
+                    self.stats["rebuild_bond"] += 1
+                    self._rebuild_from(gs)
+        if self.gather_every and self.step_no % self.gather_every == 0:
+            self.last_global = gs if gs is not None else self.global_state()
         return rec
+
+    # -- a unit joined across the cut moves to one owner ---------------------
+    def _transfer(self, joined: list) -> bool:
+        """Collective (every rank, the same `joined`): give each joined unit to
+        the owner of its lowest-index member, keeping every window.  False if
+        the partition cannot take it (C1 / C2): the caller re-partitions."""
+        plan, L, G = self.plan, self.p.box_x, self.G
+        nodes = np.unique(np.concatenate(joined))
+        edges = [np.stack([u[:-1], u[1:]], axis=1) for u in joined if u.size > 1]
+        groups = _components(nodes, np.concatenate(edges) if edges else np.zeros((0, 2), np.int64))
+        owner2 = plan.owner.copy()
+        for u in groups:
+            owner2[u] = plan.owner[u.min()]
+        moved = np.flatnonzero(owner2 != plan.owner)
+        if moved.size == 0:
+            return True
+        # C1: the new owner holds every protein within the halo of a moved anchor
+        for g in moved:
+            if not plan.held[owner2[g]][plan.within(plan.xw[g], self.halo + 1.0)].all():
+                return False
+        # the band can change only within halo / 2 of a moved anchor
+        X = np.unique(np.concatenate([plan.within(plan.xw[g], self.band + 1.0) for g in moved]))
+        affected = sorted(set(owner2[moved].tolist()) | set(plan.owner[moved].tolist()))
+        own_x = list(plan.own_x)
+        near = list(plan.near)
+        for r in affected:
+            own_x[r] = _resorted(plan.own_x[r], plan.xw, moved, plan.owner, owner2, r)
+            nr = plan.near[r].copy()
+            hx = X[plan.held[r][X]]
+            nr[X] = False
+            nr[hx] = (owner2[hx] == r) | (periodic_dist(plan.xw[hx], own_x[r], L) < self.band)
+            near[r] = nr
+        w = self.win
+        own_loc = owner2[w.gids] == self.rank
+        band_loc = near[self.rank][w.gids] & ~own_loc
+        # C2: a protein that joins my band must have its unit held whole here:
+        # none of its links was cut at the exchange
+        newb = np.flatnonzero(band_loc & ~w.band).astype(np.int32)
+        cut = self.eng.dd_cut_count(newb) if newb.size else 0
+        if not all(self.comm.allgather(self.rank, cut == 0)):
+            return False
+        plan.owner = owner2
+        plan.own_x = own_x
+        plan.near = near
+        w.own = own_loc.astype(np.uint8)
+        w.band = band_loc
+        self._set_lists()
+        self.stats["transfers"] += 1
+        self.stats["moved"] += int(moved.size)
+        return True
 
     def _recover(self, widen: bool) -> None:
         """Back to the checkpoint, replay to the last good step, re-partition
         there (with a wider halo on a repeated failure)."""
-        self.stats["rollbacks"] += 1
-        if self.stats["rollbacks"] > 64 or self.halo > 64 * self.p.box_x:
-            raise SlabError("decomposed step does not pass its checks even with the whole box as halo")
+        self.stats["rollbacks"] += 1  # a statistic: the retries of one step are bounded in step()
         hist = self.history
         self.stats["replayed"] += len(hist)
         if widen:
@@ -609,6 +793,25 @@ class SlabRank:
             self.eng = None
 
 
+def _resorted(own_x: np.ndarray, xw: np.ndarray, moved: np.ndarray, owner: np.ndarray, owner2: np.ndarray,
+              r: int) -> np.ndarray:
+    """Rank r's sorted owned anchors after the moves (the others unchanged)."""
+    out = own_x
+    lose = moved[(owner[moved] == r) & (owner2[moved] != r)]
+    gain = moved[(owner[moved] != r) & (owner2[moved] == r)]
+    if lose.size:
+        keep = np.ones(out.size, bool)
+        for x in xw[lose]:
+            j = np.searchsorted(out, x)
+            while not keep[j]:  # equal anchors: drop the next copy
+                j += 1
+            keep[j] = False
+        out = out[keep]
+    if gain.size:
+        out = np.sort(np.concatenate([out, xw[gain]]))
+    return out
+
+
 def combine(parts) -> np.ndarray:
     """bond.dat record of the trajectory from the slabs' shares (sums; the
     largest complex by max; cluster_size as k_finalize computes it)."""
@@ -625,11 +828,13 @@ def combine(parts) -> np.ndarray:
 
 
 def run_local(p: capi.Params, hs: capi.HostState, G: int, steps: int, make_engine: Callable,
-              halo: float = 900.0, gather_every: int = 0, on_step: Optional[Callable] = None):
+              halo: float = 900.0, gather_every: int = 0, on_step: Optional[Callable] = None,
+              margin: Optional[float] = None):
     """G slabs as threads of this process (e.g. G handles on one GPU).
     Returns (records[steps], ranks).  on_step(rank0, k, rec) after each step on rank 0."""
     comm = LocalComm(G)
-    ranks = [SlabRank(p, r, comm, make_engine, halo=halo, gather_every=gather_every) for r in range(G)]
+    ranks = [SlabRank(p, r, comm, make_engine, halo=halo, gather_every=gather_every, margin=margin)
+             for r in range(G)]
     recs = np.zeros(steps, dtype=capi.OBS_DTYPE)
 
     def body(r):

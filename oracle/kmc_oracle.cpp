@@ -169,6 +169,17 @@ struct Oracle {
   int dd_off[4] = {0, 0, 0, 0};
   int64_t dd_xcol = 0, dd_xbond = 0;
   bool owned(int p) const { return !dd || dd_own[p]; }
+  // the device-resident exchange's contract (oracle_dd_plan / pack / unpack /
+  // finish, kmc_dd_* of include/kmc.h) on host memory: the plan, band and
+  // cut flags (1-based), and the step's report
+  std::vector<int32_t> dd_send, dd_recv;
+  std::vector<uint8_t> dd_band, dd_cut;
+  kmc_dd_report dd_rep{};
+  void dd_xbond_at(int i, int j) {
+    ++dd_xbond;
+    if (dd_rep.n_xb < KMC_DD_XCAP) dd_rep.xb[dd_rep.n_xb][0] = i - 1, dd_rep.xb[dd_rep.n_xb][1] = j - 1;
+    ++dd_rep.n_xb;
+  }
 
   inline size_t I(int p, int j, int k) const { return ((size_t)p * 5 + j) * 5 + k; }
   inline int& ST(int p, int j) { return st[(size_t)p * 5 + j]; }
@@ -713,7 +724,7 @@ struct Oracle {
               (kmcm::fabs_(theta_ot2 - 180) < P.bond_thetaot_cutoff)) {
             double prob = rng.pair(kmcr::DOM_RL, i, j, step, (uint32_t)k);
             if (prob < PAss) {
-              if (dd && dd_own[i] != dd_own[j]) ++dd_xbond;
+              if (dd && dd_own[i] != dd_own[j]) dd_xbond_at(i, j);
               STN(i, 2) = 1;
               STN(j, k) = 1;
               NEIN(j, k) = i;
@@ -767,7 +778,7 @@ struct Oracle {
           if (kmcm::fabs_(theta_ot2 - 180) < P.cis_thetaot_cutoff) {
             double prob = rng.pair(pass == 0 ? kmcr::DOM_MONO : kmcr::DOM_CIS, i, j, step, 0);
             if (prob < PA) {
-              if (dd && dd_own[i] != dd_own[j]) ++dd_xbond;
+              if (dd && dd_own[i] != dd_own[j]) dd_xbond_at(i, j);
               STN(i, 3) = 1;
               STN(j, 3) = 1;
               bond_num_new++;
@@ -1355,6 +1366,11 @@ int oracle_dd_set_state(oracle_t* h, const kmc_state_view* v, const int32_t* gid
   for (int k = 0; k < 4; ++k) o.dd_off[k] = ctl5[k];
   o.maxc = ctl5[4];
   o.dd_xcol = o.dd_xbond = 0;
+  o.dd_rep = kmc_dd_report{};
+  o.dd_band.assign(o.N + 1, 0);
+  o.dd_cut.assign(o.N + 1, 0);
+  o.dd_send.clear();
+  o.dd_recv.clear();
   return 0;
 }
 int oracle_dd_export(oracle_t* h, int32_t n, const int32_t* ids, double* beads, int32_t* ints) {
@@ -1443,6 +1459,107 @@ int32_t oracle_dd_jumpers(oracle_t* h, double S, int32_t cap, int32_t* ids, doub
 void oracle_dd_counters(oracle_t* h, int64_t* out) {
   out[0] = h->o->dd_xcol;
   out[1] = h->o->dd_xbond;
+}
+
+// the device-resident exchange of include/kmc.h (kmc_dd_plan / pack /
+// unpack / finish / cut_count) on host memory, same rows, same report
+int oracle_dd_plan(oracle_t* h, int32_t n_send, const int32_t* send_ids, int32_t n_recv, const int32_t* recv_ids,
+                   const uint8_t* own, const uint8_t* band) {
+  Oracle& o = *h->o;
+  for (int p = 1; p <= o.N; ++p)
+    if (own[p - 1] > 1 || band[p - 1] > 1 || (own[p - 1] && band[p - 1])) {
+      g_err = "dd: own / band flags";
+      return KMC_ERR_ARG;
+    }
+  for (int32_t i = 0; i < n_send; ++i)
+    if (send_ids[i] < 0 || send_ids[i] >= o.N || !own[send_ids[i]]) {
+      g_err = "dd: a sent protein out of range or not owned";
+      return KMC_ERR_ARG;
+    }
+  for (int32_t i = 0; i < n_recv; ++i)
+    if (recv_ids[i] < 0 || recv_ids[i] >= o.N || own[recv_ids[i]]) {
+      g_err = "dd: a received protein out of range or owned";
+      return KMC_ERR_ARG;
+    }
+  o.dd_send.assign(send_ids, send_ids + n_send);
+  o.dd_recv.assign(recv_ids, recv_ids + n_recv);
+  o.dd_band.assign(o.N + 1, 0);
+  o.dd_cut.resize(o.N + 1, 0);
+  for (int p = 1; p <= o.N; ++p) o.dd_own[p] = own[p - 1], o.dd_band[p] = band[p - 1];
+  return 0;
+}
+int oracle_dd_pack(oracle_t* h, void* dst) {
+  Oracle& o = *h->o;
+  unsigned char* rows = (unsigned char*)dst;
+  const int32_t n = (int32_t)o.dd_send.size();
+  for (int32_t t = 0; t < n; ++t) {
+    double* b = (double*)(rows + (size_t)t * KMC_DD_ROW);
+    int32_t* f = (int32_t*)(rows + (size_t)t * KMC_DD_ROW + 384);
+    oracle_dd_export(h, 1, &o.dd_send[t], b, f);
+    const bool rec = o.dd_send[t] < o.NA;
+    for (int k = 0; k < 8; ++k)
+      if ((rec ? (k == 2 || k == 4) : k >= 4) && f[k] > 0) f[k] = o.dd_gid[f[k] - 1] + 1;
+  }
+  return 0;
+}
+int oracle_dd_unpack(oracle_t* h, const void* src, int32_t first, int32_t n) {
+  Oracle& o = *h->o;
+  if (first < 0 || n < 0 || (size_t)first + n > o.dd_recv.size()) {
+    g_err = "dd: unpack range outside the receive plan";
+    return KMC_ERR_ARG;
+  }
+  const unsigned char* rows = (const unsigned char*)src;
+  for (int32_t t = 0; t < n; ++t) {
+    const int32_t id = o.dd_recv[first + t];
+    const int p = id + 1;
+    const bool rec = p <= o.NA;
+    double b[48];
+    int32_t f[8];
+    std::memcpy(b, rows + (size_t)t * KMC_DD_ROW, sizeof b);
+    std::memcpy(f, rows + (size_t)t * KMC_DD_ROW + 384, sizeof f);
+    uint32_t lost = 0;  // bit k: link field k reaches a protein the window does not hold
+    for (int k = 0; k < 8; ++k) {
+      if (!(rec ? (k == 2 || k == 4) : k >= 4) || f[k] <= 0) continue;
+      auto it = std::lower_bound(o.dd_gid.begin(), o.dd_gid.end(), f[k] - 1);
+      if (it != o.dd_gid.end() && *it == f[k] - 1) {
+        f[k] = (int32_t)(it - o.dd_gid.begin()) + 1;
+      } else {
+        f[k] = 0;
+        lost |= 1u << k;
+      }
+    }
+    // cut with the status the link carries (as the window was cut when set)
+    if (rec) {
+      if (lost & (1u << 2)) f[0] = 0, f[3] = 0;
+      if (lost & (1u << 4)) f[1] = 0;
+    } else {
+      for (int j = 0; j < 4; ++j)
+        if (lost & (1u << (4 + j))) f[j] = 0;
+    }
+    uint8_t fl = 0;
+    oracle_dd_import(h, 1, &id, b, f, &fl);
+    o.dd_cut[p] = lost != 0;
+    if (fl) ++o.dd_rep.differed;
+    if (fl & 2) ++o.dd_rep.links;
+    if (o.dd_band[p] && (fl || lost)) ++o.dd_rep.bad;
+  }
+  return 0;
+}
+int oracle_dd_finish(oracle_t* h, double S, kmc_dd_report* out) {
+  Oracle& o = *h->o;
+  o.dd_rep.n_jump = oracle_dd_jumpers(h, S, KMC_DD_JCAP, o.dd_rep.jump_id, o.dd_rep.jump_x);
+  o.dd_rep.xcol = o.dd_xcol;
+  o.dd_rep.xbond = o.dd_xbond;
+  *out = o.dd_rep;
+  o.dd_rep.bad = o.dd_rep.differed = o.dd_rep.links = o.dd_rep.n_jump = o.dd_rep.n_xb = 0;
+  return 0;
+}
+int oracle_dd_cut_count(oracle_t* h, int32_t n, const int32_t* ids, int32_t* count) {
+  Oracle& o = *h->o;
+  int32_t c = 0;
+  for (int32_t i = 0; i < n; ++i) c += (ids[i] >= 0 && ids[i] < o.N && !o.dd_cut.empty()) ? o.dd_cut[ids[i] + 1] : 0;
+  *count = c;
+  return 0;
 }
 
 uint64_t oracle_hash(oracle_t* h) { return h->o->hash(); }

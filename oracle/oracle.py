@@ -82,6 +82,12 @@ def lib():
         L.oracle_dd_counters.argtypes = [C.c_void_p, C.c_void_p]
         L.oracle_dd_jumpers.restype = C.c_int32
         L.oracle_dd_jumpers.argtypes = [C.c_void_p, C.c_double, C.c_int32, C.c_void_p, C.c_void_p]
+        L.oracle_dd_plan.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p,
+                                     C.c_void_p]
+        L.oracle_dd_pack.argtypes = [C.c_void_p, C.c_void_p]
+        L.oracle_dd_unpack.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32]
+        L.oracle_dd_finish.argtypes = [C.c_void_p, C.c_double, C.POINTER(capi.DDReport)]
+        L.oracle_dd_cut_count.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.POINTER(C.c_int32)]
         _lib = L
     return _lib
 
@@ -181,6 +187,42 @@ class Oracle:
             if n <= cap:
                 return ids[:n], xs[:n]
             cap = n
+
+    # the device-resident exchange's contract on host memory (slabs.py drives
+    # oracle windows and libkmc handles alike; addresses are host addresses)
+    device = None
+    list_growth = 0
+
+    def set_list_growth(self, level: int) -> None:
+        pass
+
+    def dd_plan(self, send_ids, recv_ids, own, band) -> None:
+        send_ids = np.ascontiguousarray(send_ids, dtype=np.int32)
+        recv_ids = np.ascontiguousarray(recv_ids, dtype=np.int32)
+        own = np.ascontiguousarray(own, dtype=np.uint8)
+        band = np.ascontiguousarray(band, dtype=np.uint8)
+        self._check(lib().oracle_dd_plan(self.h, send_ids.size, send_ids.ctypes.data, recv_ids.size,
+                                         recv_ids.ctypes.data, own.ctypes.data, band.ctypes.data))
+        self._sendbuf = np.zeros(max(1, send_ids.size) * capi.DD_ROW, dtype=np.uint8)
+
+    def dd_pack(self, dst: int = 0) -> int:
+        dst = dst or self._sendbuf.ctypes.data
+        self._check(lib().oracle_dd_pack(self.h, dst))
+        return dst
+
+    def dd_unpack(self, src: int, first: int, n: int) -> None:
+        self._check(lib().oracle_dd_unpack(self.h, src, first, n))
+
+    def dd_finish(self, S: float):
+        rep = capi.DDReport()
+        self._check(lib().oracle_dd_finish(self.h, S, C.byref(rep)))
+        return rep
+
+    def dd_cut_count(self, ids) -> int:
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        c = C.c_int32()
+        self._check(lib().oracle_dd_cut_count(self.h, ids.size, ids.ctypes.data, C.byref(c)))
+        return int(c.value)
 
     def set_stream(self, clock: int, rand_calls: int):
         """Resume stream mode at rand2() clock `clock` after `rand_calls` rand()s."""

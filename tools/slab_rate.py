@@ -1,18 +1,24 @@
 """Step rate of one trajectory split into G slabs (slabs.py) against the
-single-handle engine on the same GPU, from the same placement (diagnostic
-measurement, not the bench: the slab driver exchanges halos through the host
-every step).
-  python -u tools/slab_rate.py [workload] [G ...] [--steps K] [--procs]
-Prints per G: ms/step, the driver's counters (units exchanged / verified per
-step, re-partitions, rollbacks) and the single-handle ms/step.  --procs: the
-G ranks as processes (torch.distributed over gloo, TorchComm, every handle on
-device 0) instead of threads of this process.
+single-handle engine on the same GPU, from the same state (diagnostic
+measurement, not the bench).
+  python -u tools/slab_rate.py [workload] [G ...] [--steps K] [--halo H]
+                               [--evolve E] [--check] [--procs]
+The state is the placement, or (--evolve E) the placement evolved E steps on
+one handle.  Per G: ms/step of the timed loop (after start(), bracketed by
+barriers on every rank), the partition time, the driver's counters and rank
+0's host seconds per phase.  --check: the G-slab records equal the single
+handle's over the same K steps, and the final states' hashes too.  --procs:
+the G ranks as processes (torch.distributed over gloo, TorchComm, every
+handle on device 0) instead of threads of this process.
 """
 import argparse
 import importlib
 import os
 import sys
+import threading
 import time
+
+import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
@@ -22,22 +28,45 @@ slabs = importlib.import_module(PKG + ".slabs")
 workloads = importlib.import_module(PKG + ".workloads")
 
 
+def initial_state(p, evolve):
+    if not evolve:
+        return engine.host_init_random(p)
+    with engine.Simulation(p) as sim:
+        sim.set_state(engine.host_init_random(p))
+        sim.step(evolve)
+        return sim.get_state()
+
+
+def phases(s, k):
+    return ", ".join(f"{n} {v / k * 1e3:.3f}" for n, v in s["sec"].items())
+
+
+def counters(s):
+    keys = ("rebuilds", "rebuild_bond", "rebuild_jumpers", "transfers", "moved", "rollbacks", "xbond", "held", "owned")
+    return ", ".join(f"{k} {s[k]}" for k in keys)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("workload", nargs="?", default="C2")
     ap.add_argument("G", nargs="*", type=int, default=[2, 4])
     ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--halo", type=float, default=900.0)
+    ap.add_argument("--evolve", type=int, default=0)
+    ap.add_argument("--check", action="store_true")
     ap.add_argument("--procs", action="store_true")
     a = ap.parse_args()
     p = workloads.params(a.workload, seed=1)
-    st = engine.host_init_random(p)
+    st = initial_state(p, a.evolve)
+    K = a.steps
     with engine.Simulation(p) as sim:
         sim.set_state(st)
-        sim.step(10)
-        t = time.time()
-        sim.step(a.steps)
-        one = (time.time() - t) / a.steps * 1e3
-    print(f"{a.workload} single handle: {one:.3f} ms/step", flush=True)
+        t = time.perf_counter()
+        ref = sim.step(K).copy()
+        one = (time.perf_counter() - t) / K * 1e3
+        ref_h = engine.state_hash(p, sim.get_state()) if a.check else None
+    print(f"{a.workload} (step {st.step}, {int(st.counters[0])} bonds) single handle: {one:.3f} ms/step over {K} "
+          f"steps (from the set state)", flush=True)
     if a.procs:
         import socket
 
@@ -47,36 +76,52 @@ def main():
             with socket.socket() as so:
                 so.bind(("127.0.0.1", 0))
                 port = so.getsockname()[1]
-            mp.spawn(_proc_rank, args=(G, port, a.workload, a.steps), nprocs=G, join=True)
+            mp.spawn(_proc_rank, args=(G, port, a.workload, K, a.halo, a.evolve), nprocs=G, join=True)
         return
     for G in a.G:
-        # the partition and the windows' handles (start) timed apart: two runs
-        # from the same state, of 1 and of K steps
-        tt = []
-        for k in (1, a.steps):
-            t0 = time.time()
-            recs, ranks = slabs.run_local(p, st, G, k, lambda q: engine.Simulation(q), gather_every=k)
-            tt.append(time.time() - t0)
-            s = ranks[0].stats
-            if k > 1:
-                print("  rank 0 host ms/step by phase: " + ", ".join(
-                    f"{n} {v / k * 1e3:.3f}" for n, v in s["sec"].items()), flush=True)
-            for r in ranks:
-                r.close()
-        ms = (tt[1] - tt[0]) / (a.steps - 1) * 1e3
-        print(f"{a.workload} G={G}: {ms:.3f} ms/step (start {tt[0] * 1e3:.0f} ms), exchanged "
-              f"{s['exchanged'] / a.steps:.0f} verified {s['verified'] / a.steps:.0f} units/step, rebuilds "
-              f"{s['rebuilds']}, rollbacks {s['rollbacks']}, held {s['held']} of {p.n_a + p.n_b}", flush=True)
+        comm = slabs.LocalComm(G)
+        ranks = [slabs.SlabRank(p, r, comm, lambda q: engine.Simulation(q), halo=a.halo,
+                                gather_every=K if a.check else 0) for r in range(G)]
+        recs = np.zeros(K, dtype=engine.capi.OBS_DTYPE)
+        clock = {}
+        bar = threading.Barrier(G)
+
+        def body(r):
+            me = ranks[r]
+            t0 = time.perf_counter()
+            me.start(st)
+            bar.wait()
+            t1 = time.perf_counter()
+            for k in range(K):
+                rec = me.step()
+                if r == 0:
+                    recs[k] = rec[0]
+            bar.wait()
+            if r == 0:
+                clock.update(start=t1 - t0, loop=time.perf_counter() - t1)
+
+        body.comms = [comm]
+        slabs.run_threads(G, body)
+        s = ranks[0].stats
+        msg = (f"{a.workload} G={G} halo {a.halo:.0f}: {clock['loop'] / K * 1e3:.3f} ms/step over {K} steps "
+               f"(start {clock['start'] * 1e3:.0f} ms); {counters(s)}")
+        if a.check:
+            same = np.array_equal(recs, ref) and engine.state_hash(p, ranks[0].last_global) == ref_h
+            msg += f"; equal to the single handle: {same}"
+        print(msg, flush=True)
+        print(f"  rank 0 host ms/step by phase: {phases(s, K)}", flush=True)
+        for r in ranks:
+            r.close()
 
 
-def _proc_rank(rank, G, port, workload, steps):
+def _proc_rank(rank, G, port, workload, steps, halo, evolve):
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=G)
     p = workloads.params(workload, seed=1)
-    st = engine.host_init_random(p)
-    me = slabs.SlabRank(p, rank, slabs.TorchComm(), lambda q: engine.Simulation(q, device=0), gather_every=0)
+    st = initial_state(p, evolve)
+    me = slabs.SlabRank(p, rank, slabs.TorchComm(), lambda q: engine.Simulation(q, device=0), halo=halo)
     t0 = time.time()
     me.start(st)
     dist.barrier()
@@ -87,9 +132,9 @@ def _proc_rank(rank, G, port, workload, steps):
     t2 = time.time()
     if rank == 0:
         s = me.stats
-        print(f"{workload} G={G} processes: {(t2 - t1) / steps * 1e3:.3f} ms/step (start {(t1 - t0) * 1e3:.0f} ms), "
-              f"rebuilds {s['rebuilds']}, rollbacks {s['rollbacks']}; rank 0 host ms/step by phase: " +
-              ", ".join(f"{n} {v / steps * 1e3:.3f}" for n, v in s["sec"].items() if n != "rebuild"), flush=True)
+        print(f"{workload} G={G} processes: {(t2 - t1) / steps * 1e3:.3f} ms/step (start {(t1 - t0) * 1e3:.0f} ms); "
+              f"{counters(s)}", flush=True)
+        print(f"  rank 0 host ms/step by phase: {phases(s, steps)}", flush=True)
     me.close()
     dist.destroy_process_group()
 
