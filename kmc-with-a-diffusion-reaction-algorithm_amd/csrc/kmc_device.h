@@ -31,6 +31,11 @@ struct KParams {
   // ligand pair (2RB) / ligand–receptor pair (RA + RB + 0.3 Å) may collide, + 2.5 Å for the rounding
   float ref_bb, ref_ab;
   int col_refine;  // 1 (default; KMC_COL_REFINE=0 turns it off: the same results, more fp64 gathers)
+  // the R–L reaction tests' refinement from the records (rxn_refine): squared float distance below which a
+  // ligand site may lie within bond_cut of the receptor's site (+ 3 Å for the records' rounding); on unless
+  // KMC_RXN_REFINE=0 or a set state's binding sites are not where the templates put them (sites_ok)
+  float ref_rl;
+  int rxn_refine;
   kmcr::Key key;
   int tcap;  // LDS tile record capacity (<= TCAP; lowered only to test the global path)
   int tile;  // cells per tile side of the LDS scans (<= TILE_MAX)
@@ -76,8 +81,8 @@ struct Ctl {
   uint32_t last_outl;     // diagnostics: the previous step's outlier records (n_outl)
   uint32_t cand_kind[6];  // diagnostics (KMC_DEBUG_CAND) since the state was set: collision candidates
                           // of kind pair A-A, A-B, B-B (proposal kind + other kind), tested / colliding
-  uint32_t rxn_kind[4];   // diagnostics (KMC_DEBUG_CAND): reaction pairs tested, final-final, within the
-                          // first distance gate, accepting
+  uint32_t rxn_kind[5];   // diagnostics (KMC_DEBUG_CAND): reaction pairs tested, final-final, within the
+                          // first distance gate, accepting; R–L site tests the record refinement ruled out
   uint64_t vtag;          // BFS tag counter for the overflow path
   uint64_t stamps[24];    // diagnostic build (-DKMC_STAMPS) only: phase cycles (tile scans, complexes)
   // decomposed trajectories (KParams::dd), since kmc_dd_set_state: collisions found between a unit this

@@ -333,6 +333,7 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
   K.T_cis = sqrt_threshold(p->cis_dist_cutoff);
   K.ref_bb = (float)((2 * p->rb_radius + 2.5) * (2 * p->rb_radius + 2.5));
   K.ref_ab = (float)((p->ra_radius + p->rb_radius + 0.3 + 2.5) * (p->ra_radius + p->rb_radius + 0.3 + 2.5));
+  K.ref_rl = (float)((p->bond_dist_cutoff + 3.0) * (p->bond_dist_cutoff + 3.0));
   {
     const char* cr = getenv("KMC_COL_REFINE");
     K.col_refine = !(cr && *cr == '0');
@@ -694,9 +695,45 @@ int kmc_set_state(kmc_sim* s, const kmc_state_view* v) {
   return set_state_impl(s, v);
 }
 
+// The binding sites where the templates put them (main.cpp:303-311, 392-410,
+// 1157-1178; every later move is rigid): a receptor's [3][2] = 2·[3][1] −
+// [3][3] at RA from [3][1], a ligand's site [k][2] on the line from its
+// centre through subunit [k][1] at (1 + √3/2) times the subunit's offset —
+// each within 0.5 Å.  rxn_refine relies on both; a state that breaks them
+// (a hand-made position.cpt) runs without it.
+static bool sites_ok(const kmc_params* p, const kmc_state_view* v) {
+  const int NA = p->n_a, NB = p->n_b;
+  auto A = [&](int i, int j, int k, int c) { return v->ra[((size_t)((j - 1) * 4 + (k - 1)) * 3 + c) * NA + i]; };
+  auto B = [&](int b, int j, int k, int c) { return v->rb[((size_t)((j - 1) * 2 + (k - 1)) * 3 + c) * NB + b]; };
+  const double f = 1.0 + std::sqrt(3.0) / 2.0;
+  for (int i = 0; i < NA; ++i) {
+    double e = 0, r = 0;
+    for (int c = 0; c < 3; ++c) {
+      const double d = A(i, 3, 2, c) - (2 * A(i, 3, 1, c) - A(i, 3, 3, c)), q = A(i, 3, 2, c) - A(i, 3, 1, c);
+      e += d * d;
+      r += q * q;
+    }
+    if (!(e <= 0.25) || !(std::fabs(std::sqrt(r) - p->ra_radius) <= 0.5)) return false;
+  }
+  for (int b = 0; b < NB; ++b)
+    for (int k = 2; k <= 4; ++k) {
+      double e = 0;
+      for (int c = 0; c < 3; ++c) {
+        const double d = B(b, k, 2, c) - (B(b, 1, 1, c) + f * (B(b, k, 1, c) - B(b, 1, 1, c)));
+        e += d * d;
+      }
+      if (!(e <= 0.25)) return false;
+    }
+  return true;
+}
+
 static int set_state_impl(kmc_sim* s, const kmc_state_view* v) {
   int rc = kmch_host::validate(&s->p, v, &s->err);
   if (rc != KMC_OK) return rc;
+  {
+    const char* rr = getenv("KMC_RXN_REFINE");
+    s->K.rxn_refine = !(rr && *rr == '0') && sites_ok(&s->p, v);
+  }
   const int NA = s->p.n_a, NB = s->p.n_b;
   Dev& d = s->d;
   // beads arrive in the host layout: into the scratch buffers, converted to
@@ -1217,8 +1254,9 @@ int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out) {
       if (s->K.dbg_cand) {
         const uint32_t* c = s->ctl_host->cand_kind;
         const uint32_t* r = s->ctl_host->rxn_kind;
-        fprintf(stderr, "kmc cand AA %u/%u AB %u/%u BB %u/%u (tested/colliding) rxn %u final %u gate %u accept %u\n",
-                c[0], c[1], c[2], c[3], c[4], c[5], r[0], r[1], r[2], r[3]);
+        fprintf(stderr, "kmc cand AA %u/%u AB %u/%u BB %u/%u (tested/colliding) rxn %u final %u gate %u accept %u "
+                "refined-out %u\n",
+                c[0], c[1], c[2], c[3], c[4], c[5], r[0], r[1], r[2], r[3], r[4]);
       }
       const uint64_t* t = s->ctl_host->stamps;
       if (t[16])

@@ -3952,6 +3952,36 @@ __global__ void __launch_bounds__(PAIR_THREADS, PAIR_WAVES) k_pair_scan(KParams 
 // accepting edge when its keyed draw is below the acceptance probability.
 // The greedy kernels below replay the reference's loop order on the edges.
 // (workgroup blk of nblk taking part)
+// Refinement of an R–L reaction pair from the two records (float,
+// conservative, before any fp64 gather): bit k − 2 set if the ligand's site
+// [k][2] (k = 2..4) may lie within bond_cut of the receptor's site [3][2]
+// (main.cpp:1880-1884).  The ligand's sites are (1 + √3/2) times its subunit
+// offsets from the centre (main.cpp:392-410), which the record carries to
+// 0.87 Å (lig_pack): ≤ 1.62 Å off.  The receptor's [3][2] = 2·[3][1] − [3][3]
+// (main.cpp:303-311): its xy from the axis (record x, y; [3][1] within 0.3 Å
+// of it) and the [3][3] site xy in the record, ≤ 0.6 Å off; its z within RA
+// (+ 0.3) of the domains' z span.  Margin 3 Å (P.ref_rl); sites_ok checks the
+// templates' geometry when a state is set.  At C5, 95 % of the final-final R–L
+// pairs fail the first gate (profiles/r05/c5_window_r5o_debug_counters.log).
+__device__ __forceinline__ uint32_t rxn_refine(const KParams& P, const Rec& R, const Rec& L) {
+  const uint32_t w0 = __float_as_uint(L.pos.w), w1 = __float_as_uint(L.site.x), w2 = __float_as_uint(L.site.y);
+  if ((w2 >> 8) & 1u) return 7u;  // an offset out of the byte range: no refinement
+  const uint32_t b[9] = {w0, w0 >> 8, w0 >> 16, w0 >> 24, w1, w1 >> 8, w1 >> 16, w1 >> 24, w2};
+  const float f = 1.8660254f;
+  const float sx = 2.0f * R.pos.x - R.site.x, sy = 2.0f * R.pos.y - R.site.y;
+  const float zlo = R.pos.z - ((float)P.ra + 0.3f), zhi = R.pos.w + ((float)P.ra + 0.3f);
+  uint32_t m = 0;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const float dx = L.pos.x + f * (float)(int8_t)(b[3 * j] & 0xff) - sx;
+    const float dy = L.pos.y + f * (float)(int8_t)(b[3 * j + 1] & 0xff) - sy;
+    const float z = L.pos.z + f * (float)(int8_t)(b[3 * j + 2] & 0xff);
+    const float dz = fmaxf(fmaxf(z - zhi, zlo - z), 0.0f);
+    m |= (dx * dx + dy * dy + dz * dz < P.ref_rl ? 1u : 0u) << j;
+  }
+  return m;
+}
+
 __device__ __forceinline__ void rxn_exact(const KParams& P, const Dev& d, uint32_t blk, uint32_t nblk) {
   const int NA = P.NA, NB = P.NB;
   const uint32_t step = d.ctl->step;
@@ -3971,7 +4001,10 @@ __device__ __forceinline__ void rxn_exact(const KParams& P, const Dev& d, uint32
     const Beads& NQ = rb.x < 0 ? d.nxt : d.cur;
     if (q >= NA) {
       int lb = q - NA;
+      const uint32_t may = P.rxn_refine ? rxn_refine(P, d.rec[pr.x], d.rec[pr.y]) : 7u;
+      if (P.dbg_cand && may != 7u) atomicAdd(&d.ctl->rxn_kind[4], 3u - (uint32_t)__popc(may));
       for (int k = 2; k <= 4; ++k) {
+        if (!((may >> (k - 2)) & 1u)) continue;
         if (B_ST(d, lb, k) != 0) continue;
         double ddx = NQ.B(lb, k, 2, 0) - NI.A(i, 3, 2, 0), ddy = NQ.B(lb, k, 2, 1) - NI.A(i, 3, 2, 1),
                ddz = NQ.B(lb, k, 2, 2) - NI.A(i, 3, 2, 2);

@@ -107,15 +107,20 @@ class LocalComm:
 
     def __init__(self, world: int):
         self.world = world
-        self._slots: list = [None] * world
+        # two slot arrays used in turn: a rank writes the next call's slots
+        # only after the barrier of this call, and the call after that (same
+        # slots) only after every rank has passed the next call's barrier —
+        # so one barrier per call suffices
+        self._slots = [[None] * world, [None] * world]
+        self._turn = [0] * world
         self._bar = threading.Barrier(world)
 
     def allgather(self, rank: int, obj):
-        self._slots[rank] = obj
+        slots = self._slots[self._turn[rank]]
+        self._turn[rank] ^= 1
+        slots[rank] = obj
         self._bar.wait()
-        out = list(self._slots)
-        self._bar.wait()
-        return out
+        return list(slots)
 
     def exchange(self, rank: int, me: "SlabRank") -> None:
         ptr = me.eng.dd_pack() if me.eng_ok else None
