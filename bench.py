@@ -75,6 +75,11 @@ TRAFFIC_JSON = "profiles/traffic_C3.json"
 # the proposal phase the engine brackets as "k_propose" (kmc_engine.hip
 # launch_step): these kernels back to back on the engine's stream
 PROPOSE_PHASE = ("k_bfs", "k_propose_free", "k_move_members", "k_cx_check", "k_complex_heavy")
+# single kernels reported beside the phase: the largest one of
+# the step (HBM-bound, judged by its counter traffic: its algorithmic bytes
+# depend on how many proteins are in complexes) and the furthest below the
+# roofline (issue-bound, judged by its algorithmic bytes)
+DETAIL_KERNELS = ("k_propose_free", "k_pair_scan")
 
 
 def pmc_traffic(kernel: str, workload: str):
@@ -328,7 +333,7 @@ def run_rank(args, rank: int, world: int, local: int):
     breakdown = {k: round(v[0] / max(v[1], 1), 4) for k, v in sorted(kt.items(), key=lambda x: -x[1][0])}
     # timed region: only the dominant kernel is bracketed, in every 8th step
     # (an event pair adds a few microseconds of queue time to its step)
-    sim.set_timing([dom], every=TIMING_EVERY)
+    sim.set_timing([dom, *[k for k in DETAIL_KERNELS if k != dom]], every=TIMING_EVERY)
     dt_local, (sums, maxima, cluster) = timed(args.steps)
     dt, per_rank = max_over_ranks(dt_local)
 
@@ -341,8 +346,26 @@ def run_rank(args, rank: int, world: int, local: int):
     if world == 1:
         reduce_info["equals_local"] = bool((sums == own_s).all() and (maxima == own_m).all())
 
-    total_ms, launches = sim.kernel_times().get(dom, (0.0, 0))
+    ktimed = sim.kernel_times()
+    total_ms, launches = ktimed.get(dom, (0.0, 0))
     avg_s = total_ms / 1e3 / max(launches, 1)
+    detail = {}
+    for k in DETAIL_KERNELS:
+        ms, nl = ktimed.get(k, (0.0, 0))
+        if not nl:
+            continue
+        a_s = ms / 1e3 / nl
+        kb_k = kernel_bytes(k, p.n_a, p.n_b)
+        tr_k = pmc_traffic(k, args.workload)
+        detail[k] = {
+            "avg_launch_ms": a_s * 1e3,
+            "bytes_per_launch": kb_k,
+            "achieved": (kb_k / a_s / 1e9) if kb_k else None,
+            "frac": (kb_k / a_s / 1e9 / HBM_PEAK_GBS) if kb_k else None,
+            "traffic": tr_k,
+            "achieved_by_traffic": (tr_k / a_s / 1e9) if tr_k else None,
+            "frac_by_traffic": (tr_k / a_s / 1e9 / HBM_PEAK_GBS) if tr_k else None,
+        }
     kb = kernel_bytes(dom, p.n_a, p.n_b)
     achieved = (kb / avg_s / 1e9) if (kb and avg_s > 0) else None
     traffic = pmc_traffic(dom, args.workload)
@@ -407,6 +430,7 @@ def run_rank(args, rank: int, world: int, local: int):
                 "avg_launch_ms": avg_s * 1e3,
                 "step_bytes": step_b,
                 "step_frac": step_b / (ms_per_step / 1e3) / 1e9 / HBM_PEAK_GBS,
+                "by_kernel": detail,
             },
             "cpu_baseline": cpu,
             "ensemble_reduce": reduce_info,

@@ -1188,8 +1188,17 @@ struct Stamper {
 // reference's kind tests carry over unchanged: receptor t -> t, ligand t ->
 // NA + t.  Larger complexes (rare) run the same code on global memory.
 #define CX_SHUF 6  // random_shuffle passes whose draws are precomputed (4 + 2 repeats of lable4)
+// Member stride of the LDS image in doubles.  48 (384 B) put the same
+// coordinate of every member on one bank — 96 dwords ≡ 0 mod 32 — so the
+// steps that take one member per lane (the alignment's member loops, the
+// records, the extent bound) were 16-way conflicted (SQ_LDS_BANK_CONFLICT 41 %
+// of the kernel's LDS cycles at C3, profiles/r05/final_C3); 49 (392 B, 98
+// dwords) spreads a 16-lane group over 16 bank pairs.
+#ifndef CX_STRIDE
+#define CX_STRIDE 49
+#endif
 struct CxLds {
-  double bead[CXL][48];  // R_new of member t: receptor bead (j,k) at ((j-1)*4+(k-1))*3+c, ligand ((j-1)*2+(k-1))*3+c
+  double bead[CXL][CX_STRIDE];  // R_new of member t: receptor bead (j,k) at ((j-1)*4+(k-1))*3+c, ligand ((j-1)*2+(k-1))*3+c
   int lk[CXL][4];        // links (encoded): receptor {nei4 (site), nei2, nei3, -}, ligand {-, nei2, nei3, nei4}
   int slot[CXL];         // slot of member t
   int res[CXL];          // member row (encoded), shuffled in place like results[c][.]

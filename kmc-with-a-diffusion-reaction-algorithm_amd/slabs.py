@@ -479,6 +479,9 @@ class SlabRank:
         self.stats["sec"]["rebuild"] += time.perf_counter() - t0
 
     def _rebuild_inner(self, hs: capi.HostState) -> None:
+        sub = self.stats.setdefault("rebuild_sec", dict(plan=0.0, window=0.0, create=0.0, set_state=0.0,
+                                                        lists=0.0))
+        t0 = time.perf_counter()
         self.ckpt = hs.copy()
         self.ckpt.counters[:] = self.counters
         self.ckpt.step = self.step_no
@@ -486,10 +489,12 @@ class SlabRank:
         self.plan = make_plan(self.p, hs, self.G, self.halo, self.margin)
         w = self.plan.windows[self.rank]
         self.win = w
+        t1 = time.perf_counter()
         ws = window_state(hs, w)
         rl, mono, cis = derived_counts(hs)
         c = self.counters
         ctl5 = [c[0] - (rl + mono + cis), c[1] - rl, c[2] - cis, c[3] - mono, c[4]] if self.rank == 0 else [0] * 5
+        t2 = time.perf_counter()
         if self.eng is not None:
             self.eng.close()
             self.eng = None
@@ -499,11 +504,17 @@ class SlabRank:
         self.eng = self.make_engine(q)
         if self.grow:
             self.eng.set_list_growth(self.grow)
+        t3 = time.perf_counter()
         self.eng.dd_set_state(ws, w.gids, w.own, ctl5)
+        t4 = time.perf_counter()
         self.eng_ok = True
         self._xc = (0, 0)
         self._njump = 0
         self._set_lists()
+        t5 = time.perf_counter()
+        for k, a, b in (("plan", t0, t1), ("window", t1, t2), ("create", t2, t3), ("set_state", t3, t4),
+                        ("lists", t4, t5)):
+            sub[k] += b - a
         self.stats["rebuilds"] += 1
 
     def _set_lists(self) -> None:
