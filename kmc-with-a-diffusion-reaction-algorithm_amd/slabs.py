@@ -337,33 +337,54 @@ class Plan:
         return np.concatenate(idx) if len(idx) > 1 else idx[0]
 
 
+def _dist_to_set(xs: np.ndarray, mask: np.ndarray, L: float) -> np.ndarray:
+    """Periodic distance of every sorted anchor xs[i] to the nearest xs[j]
+    with mask[j] (0 for the members themselves): the nearest member at or
+    below and at or above each position by running max / min of the member
+    positions — O(N), no search."""
+    n = xs.size
+    if not mask.any():
+        return np.full(n, np.inf)
+    idx = np.arange(n)
+    prev = np.maximum.accumulate(np.where(mask, idx, -1))
+    nxt = np.minimum.accumulate(np.where(mask, idx, n)[::-1])[::-1]
+    first, last = int(np.argmax(mask)), n - 1 - int(np.argmax(mask[::-1]))
+    xp = np.where(prev >= 0, xs[np.maximum(prev, 0)], xs[last] - L)  # across the seam: the last member − L
+    xn = np.where(nxt < n, xs[np.minimum(nxt, n - 1)], xs[first] + L)
+    return np.minimum(xs - xp, xn - xs)
+
+
 def make_plan(p: capi.Params, hs: capi.HostState, G: int, halo: float, margin: float = 0.0) -> Plan:
     L = p.box_x
-    n_a = hs.n_a
+    n_a, n = hs.n_a, hs.n_a + hs.n_b
     xw = wrap(ref_x(hs), L)
     lab = units(hs)
     slab = np.clip(np.floor((xw[lab] + L / 2) / (L / G)).astype(np.int64), 0, G - 1)  # by the unit's lead
     owner = slab
     band_w = halo / 2
     order = np.argsort(xw, kind="stable")
+    xs = xw[order]
     windows, own_x, near, held_all = [], [], [], []
     for r in range(G):
         own = owner == r
-        ref = np.sort(xw[own])
-        own_x.append(ref)
-        d = periodic_dist(xw, ref, L)
+        own_s = own[order]
+        own_x.append(xs[own_s])
+        d = np.empty(n)
+        d[order] = _dist_to_set(xs, own_s, L)
         held = own | (d < halo + margin)
         band = ~own & (d < band_w)
         near.append(own | band)
         # a band protein's whole unit is held: its local computation then
         # sees every member (a unit is moved and decided as one)
-        held |= np.isin(lab, np.unique(lab[band]))
+        mark = np.zeros(n, dtype=bool)
+        mark[lab[band]] = True
+        held |= mark[lab]
         held_all.append(held)
         gids = np.flatnonzero(held).astype(np.int32)
         w = Window(gids=gids, own=own[gids].astype(np.uint8), band=band[gids],
                    n_a=int((gids < n_a).sum()), n_b=int((gids >= n_a).sum()))
         windows.append(w)
-    return Plan(owner=owner, windows=windows, halo=halo, xw=xw, xs=xw[order], xs_order=order, held=held_all,
+    return Plan(owner=owner, windows=windows, halo=halo, xw=xw, xs=xs, xs_order=order, held=held_all,
                 own_x=own_x, near=near, L=L)
 
 
@@ -425,7 +446,7 @@ class SlabRank:
     handle with the kmc_dd_* methods for a window's proteins."""
 
     def __init__(self, p: capi.Params, rank: int, comm, make_engine: Callable, halo: float = 900.0,
-                 gather_every: int = 0, margin: Optional[float] = None):
+                 gather_every: int = 0, margin: Optional[float] = None, lead: Optional[float] = None):
         self.p = p
         self.rank = rank
         self.comm = comm
@@ -435,6 +456,7 @@ class SlabRank:
         # the window holds `margin` Å beyond the halo, so that a unit joined
         # across the cut can move to its new owner without a re-partition (C1)
         self.margin = float(400.0 if margin is None else margin)
+        self._lead = lead  # None: min(200, S / 2); 0: no pre-emptive re-partition (tests of the rollback)
         self.gather_every = gather_every  # assemble the global state every k steps (tests: 1)
         self.eng = None
         self.eng_ok = True
@@ -603,21 +625,36 @@ class SlabRank:
             self._rebuild_from(self.global_state())
         return self._step_exchange()
 
-    def _jumper_check(self, ids: np.ndarray, xs: np.ndarray) -> int:
-        """Jumpers of my slab violating J_A / J_B (module docstring): count."""
+    @property
+    def lead(self) -> float:
+        """How far ahead of a failure the jumper checks re-partition: a protein
+        moves at most this far in one step (association snaps and lay-downs ≈
+        180 Å), so a jumper that passes the checks with S − lead
+        passes them with S after the next step."""
+        return min(200.0, self.S / 2) if self._lead is None else self._lead
+
+    def _jumper_check(self, ids: np.ndarray, xs: np.ndarray):
+        """Jumpers of my slab violating J_A / J_B (module docstring) with S,
+        and with S − lead: (failures, warnings)."""
         if ids.size == 0:
-            return 0
+            return 0, 0
         L = self.p.box_x
         xw = wrap(xs, L)
         g = self.win.gids[ids]
-        bad = int((periodic_dist(xw, self.plan.own_x[self.rank], L) > self.S).sum())  # J_B
+        dj = periodic_dist(xw, self.plan.own_x[self.rank], L)
+        fail, warn = dj > self.S, dj > self.S - self.lead  # J_B
         for r in range(self.G):
             if r == self.rank:
                 continue
             far = ~self.plan.near[r][g]
             if far.any():
-                bad += int((periodic_dist(xw[far], self.plan.own_x[r], L) < R_INT + self.S).sum())  # J_A
-        return bad
+                dr = periodic_dist(xw[far], self.plan.own_x[r], L)
+                fail[far] |= dr < R_INT + self.S  # J_A
+                warn[far] |= dr < R_INT + self.S + self.lead
+        if fail.any():  # (diagnostics: global index, anchor, x now)
+            self._jfail = [(int(a), round(float(self.plan.xw[a]), 1), round(float(b), 1))
+                           for a, b in zip(g[fail][:4], xw[fail][:4])]
+        return int(fail.sum()), int(warn.sum())
 
     def _cross_units(self, rep) -> Optional[list]:
         """The units joined by this step's cross-slab bonds, as sorted global
@@ -666,7 +703,7 @@ class SlabRank:
         self.comm.exchange(self.rank, self)
         t2 = time.perf_counter()
         sec["exchange"] += t2 - t1
-        bad = jbad = nj = 0
+        bad = jbad = jwarn = nj = 0
         dcol = dbond = 0
         xunits: Optional[list] = []
         if self.eng_ok:
@@ -679,7 +716,7 @@ class SlabRank:
             self.stats["exchanged"] += self.n_recv
             self.stats["verified"] += self.n_verify
             nj = rep.n_jump
-            jbad = self._jumper_check(*rep.jumpers())
+            jbad, jwarn = self._jumper_check(*rep.jumpers())
             xunits = self._cross_units(rep)
             if self.check:
                 from . import engine as _engine
@@ -692,7 +729,7 @@ class SlabRank:
         t5 = time.perf_counter()
         # the step's record from every slab's share, the checks and triggers:
         # every rank decides alike
-        shares = self.comm.allgather(self.rank, (part, bad, jbad, dbond, dcol, nj, xunits, fail, err))
+        shares = self.comm.allgather(self.rank, (part, bad, jbad, dbond, dcol, nj, xunits, fail, err, jwarn))
         sec["gather"] += time.perf_counter() - t5
         errs = [s[8] for s in shares if s[8]]
         if errs:
@@ -702,7 +739,9 @@ class SlabRank:
             return None
         if any(s[1] or s[2] for s in shares):
             self.stats["why"].append((self.step_no + 1, "verify" if any(s[1] for s in shares) else "jumper",
-                                      sum(s[1] for s in shares), sum(s[2] for s in shares)))
+                                      sum(s[1] for s in shares), sum(s[2] for s in shares),
+                                      getattr(self, "_jfail", None)))
+            self._jfail = None
             return None
         self.stats["xbond"] += sum(s[3] for s in shares)
         self.stats["xcol"] += sum(s[4] for s in shares)
@@ -728,6 +767,12 @@ class SlabRank:
                     gs = self.global_state()
                     self.stats["rebuild_bond"] += 1
                     self._rebuild_from(gs)
+        if gs is None and any(s[9] for s in shares):
+            # a jumper within one step's reach of failing its checks: re-partition
+            # now rather than roll back later
+            gs = self.global_state()
+            self.stats["rebuild_jumpers"] += 1
+            self._rebuild_from(gs)
         if self.gather_every and self.step_no % self.gather_every == 0:
             self.last_global = gs if gs is not None else self.global_state()
         return rec
@@ -845,11 +890,11 @@ def combine(parts) -> np.ndarray:
 
 def run_local(p: capi.Params, hs: capi.HostState, G: int, steps: int, make_engine: Callable,
               halo: float = 900.0, gather_every: int = 0, on_step: Optional[Callable] = None,
-              margin: Optional[float] = None):
+              margin: Optional[float] = None, lead: Optional[float] = None):
     """G slabs as threads of this process (e.g. G handles on one GPU).
     Returns (records[steps], ranks).  on_step(rank0, k, rec) after each step on rank 0."""
     comm = LocalComm(G)
-    ranks = [SlabRank(p, r, comm, make_engine, halo=halo, gather_every=gather_every, margin=margin)
+    ranks = [SlabRank(p, r, comm, make_engine, halo=halo, gather_every=gather_every, margin=margin, lead=lead)
              for r in range(G)]
     recs = np.zeros(steps, dtype=capi.OBS_DTYPE)
 

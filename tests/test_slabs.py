@@ -49,10 +49,10 @@ def whole_box(p, st, steps):
     return o.step(steps)
 
 
-def run_and_compare(p, st, G, steps, halo=900.0):
+def run_and_compare(p, st, G, steps, halo=900.0, lead=None):
     ref, hashes = whole_box(p, st, steps)
     got_h = []
-    recs, ranks = slabs.run_local(p, st, G, steps, OracleWindow, halo=halo, gather_every=1,
+    recs, ranks = slabs.run_local(p, st, G, steps, OracleWindow, halo=halo, gather_every=1, lead=lead,
                                   on_step=lambda me, k, rec: got_h.append(engine.state_hash(p, me.last_global)))
     bad = [k + 1 for k in range(steps) if recs[k] != ref[k] or got_h[k] != int(hashes[k])]
     assert not bad, f"G={G}: steps {bad[:10]} differ from the whole-box oracle"
@@ -76,10 +76,20 @@ def test_slabs_narrow_halo_recovers():
     # a halo too narrow for the step's reach (band 180 Å, S = 20 Å): jumpers
     # fail their checks and halo copies their verification — every failure
     # rolls back to the checkpoint, replays, re-partitions (widening on a
-    # repeat) and the trajectory is still the whole box's
+    # repeat) and the trajectory is still the whole box's (lead 0: no
+    # re-partition ahead of a failing jumper, so that the rollback is exercised)
+    p, st = scenario(2000, 700, 4500.0, seed=17)
+    s = run_and_compare(p, st, 2, 120, halo=360.0, lead=0.0)
+    assert s["rollbacks"] > 0 and s["replayed"] > 0, s
+
+
+def test_slabs_jumpers_repartition_ahead():
+    # the same narrow halo with the default lead: a jumper within one step's
+    # reach of failing its checks re-partitions the trajectory first, so no
+    # step has to be rolled back
     p, st = scenario(2000, 700, 4500.0, seed=17)
     s = run_and_compare(p, st, 2, 120, halo=360.0)
-    assert s["rollbacks"] > 0 and s["replayed"] > 0, s
+    assert s["rebuild_jumpers"] > 0 and s["rollbacks"] == 0, s
 
 
 def test_units_and_window_state():
@@ -156,7 +166,7 @@ def test_slabs_many_rollbacks_complete():
     p, st = scenario(2000, 700, 4500.0, seed=17)
     steps = 1000
     ref, hashes = whole_box(p, st, steps)
-    recs, ranks = slabs.run_local(p, st, 4, steps, OracleWindow, halo=330.0)
+    recs, ranks = slabs.run_local(p, st, 4, steps, OracleWindow, halo=330.0, lead=0.0)
     s = ranks[0].stats
     assert s["rollbacks"] > 64, s
     assert np.array_equal(recs, ref)

@@ -114,7 +114,8 @@ def main():
             msg += f"; equal to the single handle: {same}"
         print(msg, flush=True)
         print(f"  rank 0 host ms/step by phase: {phases(s, K)}", flush=True)
-        print(f"  checks that failed (step, kind, bad, jumper-bad): {s['why'][:8]}; most jumpers {s['jumpers']}, "
+        print(f"  checks that failed (step, kind, bad, jumper-bad, failing jumpers (gid, anchor, x)) by rank: "
+              f"{[r.stats['why'][:4] for r in ranks]}; most jumpers {s['jumpers']}, "
               f"exchanged {s['exchanged'] / K:.0f} verified {s['verified'] / K:.0f} rows/step", flush=True)
         print("  rank 0 rebuild seconds (all rebuilds): " + ", ".join(
             f"{k} {v:.3f}" for k, v in s.get("rebuild_sec", {}).items()), flush=True)
