@@ -359,7 +359,12 @@ def make_plan(p: capi.Params, hs: capi.HostState, G: int, halo: float, margin: f
     n_a, n = hs.n_a, hs.n_a + hs.n_b
     xw = wrap(ref_x(hs), L)
     lab = units(hs)
-    slab = np.clip(np.floor((xw[lab] + L / 2) / (L / G)).astype(np.int64), 0, G - 1)  # by the unit's lead
+    # by the unit's lead; the cuts sit half a slab off the periodic seam (x =
+    # ±L/2), which lies inside slab G − 1: a complex whose members straddle
+    # the seam rotates about a centre of mass far from all of them (no
+    # minimum image, main.cpp:1068-1131), so its members sweep hundreds of Å
+    # in a few dozen steps — inside a slab they fail no check
+    slab = np.floor((xw[lab] + L / 2) / (L / G) + 0.5).astype(np.int64) % G
     owner = slab
     band_w = halo / 2
     order = np.argsort(xw, kind="stable")
@@ -634,23 +639,26 @@ class SlabRank:
         return min(200.0, self.S / 2) if self._lead is None else self._lead
 
     def _jumper_check(self, ids: np.ndarray, xs: np.ndarray):
-        """Jumpers of my slab violating J_A / J_B (module docstring) with S,
-        and with S − lead: (failures, warnings)."""
+        """The listed proteins (displaced more than S − lead from their anchors):
+        (J_A / J_B failures of the jumpers proper — displaced more than S —,
+        warnings: any of them failing the checks with S − lead)."""
         if ids.size == 0:
             return 0, 0
-        L = self.p.box_x
+        L, S, lead = self.p.box_x, self.S, self.lead
         xw = wrap(xs, L)
         g = self.win.gids[ids]
+        dx = np.abs(xw - self.plan.xw[g])
+        jump = np.minimum(dx, L - dx) > S
         dj = periodic_dist(xw, self.plan.own_x[self.rank], L)
-        fail, warn = dj > self.S, dj > self.S - self.lead  # J_B
+        fail, warn = jump & (dj > S), dj > S - lead  # J_B
         for r in range(self.G):
             if r == self.rank:
                 continue
             far = ~self.plan.near[r][g]
             if far.any():
                 dr = periodic_dist(xw[far], self.plan.own_x[r], L)
-                fail[far] |= dr < R_INT + self.S  # J_A
-                warn[far] |= dr < R_INT + self.S + self.lead
+                fail[far] |= jump[far] & (dr < R_INT + S)  # J_A
+                warn[far] |= dr < R_INT + S + lead
         if fail.any():  # (diagnostics: global index, anchor, x now)
             self._jfail = [(int(a), round(float(self.plan.xw[a]), 1), round(float(b), 1))
                            for a, b in zip(g[fail][:4], xw[fail][:4])]
@@ -707,7 +715,7 @@ class SlabRank:
         dcol = dbond = 0
         xunits: Optional[list] = []
         if self.eng_ok:
-            rep = self.eng.dd_finish(self.S)
+            rep = self.eng.dd_finish(self.S - self.lead)
             t3 = time.perf_counter()
             sec["finish"] += t3 - t2
             bad = rep.bad

@@ -158,17 +158,29 @@ def test_slabs_two_processes_gloo(tmp_path):
     assert int(got["xcol"]) > 0 and int(got["exchanged"]) > 0
 
 
-def test_slabs_many_rollbacks_complete():
-    # a halo far too narrow (band 165 Å, S = 12.5 Å), four slabs: jumpers fail their checks
-    # again and again; every failure is one rollback of that step (the retries
-    # of ONE step are bounded, not the run's total), and the run completes
-    # equal to the whole box
+def test_slabs_many_rollbacks_complete(monkeypatch):
+    # every 7th step fails its checks once (an injected jumper failure): more
+    # than 64 separate rollbacks, each replayed from the checkpoint and
+    # retried from a new partition — the retries of ONE step are bounded, not
+    # the run's total — and the run completes equal to the whole box
+    orig = slabs.SlabRank._jumper_check
+
+    def forced(self, ids, xs):
+        fail, warn = orig(self, ids, xs)
+        k = self.step_no + 1
+        done = self.__dict__.setdefault("_forced", set())
+        if k % 7 == 0 and k not in done:
+            done.add(k)
+            fail += 1
+        return fail, warn
+
+    monkeypatch.setattr(slabs.SlabRank, "_jumper_check", forced)
     p, st = scenario(2000, 700, 4500.0, seed=17)
-    steps = 1000
-    ref, hashes = whole_box(p, st, steps)
-    recs, ranks = slabs.run_local(p, st, 4, steps, OracleWindow, halo=330.0, lead=0.0)
+    steps = 500
+    ref, _ = whole_box(p, st, steps)
+    recs, ranks = slabs.run_local(p, st, 2, steps, OracleWindow)
     s = ranks[0].stats
-    assert s["rollbacks"] > 64, s
+    assert s["rollbacks"] > 64 and s["replayed"] > 0, s
     assert np.array_equal(recs, ref)
 
 
