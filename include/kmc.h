@@ -242,9 +242,13 @@ int kmc_dd_counters(kmc_sim* s, int64_t* out);
  *                  of kmc_dd_set_state; band[N] = 1 for the halo proteins
  *                  whose end-of-step state must equal their owner's.  Sent
  *                  proteins must be owned, received ones not.
- *   kmc_dd_pack    the end-of-step rows of send_ids into device memory dst
+ *   kmc_dd_step    one step of the window (kmc_step) that also packs the
+ *                  end-of-step rows of send_ids into device memory dst
  *                  (n_send rows; NULL: the handle's own send buffer,
- *                  kmc_dd_send_buffer).  Returns after the stream drained.
+ *                  kmc_dd_send_buffer) and lists the owned proteins more
+ *                  than S (periodic x) from their x at kmc_dd_set_state —
+ *                  all before the step's one wait.
+ *   kmc_dd_pack    the rows alone, likewise (returns after the stream drained).
  *   kmc_dd_unpack  rows [first, first + n) of the receive plan from device
  *                  memory src (another handle's send buffer on this device,
  *                  or a collective's receive buffer), enqueued on the
@@ -256,12 +260,11 @@ int kmc_dd_counters(kmc_sim* s, int64_t* out);
  *   kmc_dd_finish  waits for the unpacks and returns the step's report: band
  *                  rows that differed or had a link cut (bad; > 0 means the
  *                  step must be redone from a wider partition), rows that
- *                  differed, rows whose status / links differed; the owned
- *                  proteins more than S (periodic x) from their x at
- *                  kmc_dd_set_state (n_jump, the first KMC_DD_JCAP listed as
- *                  local id + x); the bonds formed since the last finish
- *                  between an owned and a halo protein (n_xb, the first
- *                  KMC_DD_XCAP as local id pairs); kmc_dd_counters' values.
+ *                  differed, rows whose status / links differed; kmc_dd_step's
+ *                  jumpers (n_jump, the first KMC_DD_JCAP listed as local id
+ *                  + x); the bonds formed since the last finish between an
+ *                  owned and a halo protein (n_xb, the first KMC_DD_XCAP as
+ *                  local id pairs); kmc_dd_counters' values.
  *   kmc_dd_cut_count  how many of ids[n] had a link cut at the last unpack
  *                  (their unit is not held whole by this window).
  * A decomposed window takes no chunk snapshot (the slab driver keeps the
@@ -282,10 +285,11 @@ typedef struct kmc_dd_report {
 } kmc_dd_report;
 int kmc_dd_plan(kmc_sim* s, int32_t n_send, const int32_t* send_ids, int32_t n_recv, const int32_t* recv_ids,
                 const uint8_t* own, const uint8_t* band);
+int kmc_dd_step(kmc_sim* s, void* dst, double S, kmc_obs* out);
 int kmc_dd_pack(kmc_sim* s, void* dst);
 void* kmc_dd_send_buffer(kmc_sim* s);
 int kmc_dd_unpack(kmc_sim* s, const void* src, int32_t first, int32_t n);
-int kmc_dd_finish(kmc_sim* s, double S, kmc_dd_report* out);
+int kmc_dd_finish(kmc_sim* s, kmc_dd_report* out);
 int kmc_dd_cut_count(kmc_sim* s, int32_t n, const int32_t* ids, int32_t* count);
 
 /* Output-list capacities as 2^level times their defaults (kmc_step doubles

@@ -122,6 +122,9 @@ struct kmc_sim {
   int32_t* dd_recv_ids = nullptr;   // [dd_recv_cap]
   unsigned char* dd_sendbuf = nullptr;  // [dd_send_cap rows]
   int32_t dd_n_send = 0, dd_n_recv = 0, dd_send_cap = 0, dd_recv_cap = 0;
+  bool dd_step_pending = false;     // kmc_dd_step: pack + jumpers after the step's kernels
+  unsigned char* dd_step_dst = nullptr;
+  double dd_step_S = 0.0;
 };
 
 namespace {
@@ -1095,7 +1098,9 @@ static int launch_step_graph(kmc_sim* s) {
 // (s->step_done, or an earlier step while replaying from the snapshot);
 // device obs records land in obs_buf.  Returns after the stream has drained,
 // with the control block in ctl_host.
-static int run_chunk(kmc_sim* s, int64_t n, int64_t base) {
+static int dd_after_step(kmc_sim* s);
+
+static int run_chunk(kmc_sim* s, int64_t n, int64_t base, kmc_obs* out = nullptr) {
   HIPCHK(s, hipMemsetAsync(&s->d.ctl->obs_idx, 0, sizeof(uint32_t), s->stream));
   for (int64_t k = 0; k < n; ++k) {
     const bool rs = s->resort_every > 0 && ++s->since_resort >= s->resort_every;
@@ -1113,7 +1118,13 @@ static int run_chunk(kmc_sim* s, int64_t n, int64_t base) {
     if (rc != KMC_OK) return rc;
   }
   HIPCHK(s, hipGetLastError());
+  if (s->dd_step_pending) {  // kmc_dd_step: the exchange rows and the jumpers, before the one wait
+    const int rc = dd_after_step(s);
+    if (rc != KMC_OK) return rc;
+  }
   HIPCHK(s, hipMemcpyAsync(s->ctl_host, s->d.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, s->stream));
+  // the records in the same wait (used by the caller only if the chunk raised no error bit)
+  if (out) HIPCHK(s, hipMemcpyAsync(out, s->obs_buf, sizeof(kmc_obs_dev) * n, hipMemcpyDeviceToHost, s->stream));
   HIPCHK(s, hipStreamSynchronize(s->stream));
   if (s->tmask)
     for (int slot = 0; slot < TRING; ++slot) harvest(s, slot);
@@ -1158,11 +1169,15 @@ int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out) {
       s->snap_since = s->since_resort;
       ++s->n_snapshots;
     }
+    bool copied = false;  // the chunk's records already in `out`
     for (;;) {
-      rc = run_chunk(s, n, s->step_done);
+      rc = run_chunk(s, n, s->step_done, out ? out + done : nullptr);
       if (rc != KMC_OK) return rc;
       const uint32_t err = s->ctl_host->err;
-      if (!err) break;
+      if (!err) {
+        copied = out != nullptr;
+        break;
+      }
       // the failing step's own bits: later steps of the chunk ran on its
       // dropped entries, so their bits may be consequences
       const uint32_t cause = s->ctl_host->err_first;
@@ -1242,7 +1257,7 @@ int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out) {
       const int code = (cause & ERR_GEOMETRY) ? KMC_ERR_GEOMETRY : KMC_ERR_CAPACITY;
       return fail(s, code, m);
     }
-    if (out)
+    if (out && !copied)
       HIPCHK(s, hipMemcpy(out + done, s->obs_buf, sizeof(kmc_obs_dev) * n, hipMemcpyDeviceToHost));
     s->step_done += n;
     s->clusters_valid = true;
@@ -1503,9 +1518,14 @@ __global__ void k_dd_jumpers(KParams P, Dev d, double S, int cap, int32_t* ids, 
   }
 }
 
-// the same list into the step's report (kmc_dd_finish)
+// the same list into the step's report (kmc_dd_step; read by kmc_dd_finish),
+// with the step's collision / bond counters
 __global__ void k_dd_jumpers_rep(KParams P, Dev d, double S) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p == 0) {
+    d.dd_rep->xcol = d.ctl->dd_xcol;
+    d.dd_rep->xbond = d.ctl->dd_xbond;
+  }
   if (p >= P.N) return;
   const int r = d.id_of[p];
   if (!d.dd_own[r]) return;
@@ -1877,22 +1897,37 @@ int kmc_dd_unpack(kmc_sim* s, const void* src, int32_t first, int32_t n) {
   return KMC_OK;
 }
 
-int kmc_dd_finish(kmc_sim* s, double S, kmc_dd_report* out) {
+// (run_chunk, a kmc_dd_step's chunk) the plan's rows into the pack
+// destination and the jumpers into the report, on the stream after the step
+static int dd_after_step(kmc_sim* s) {
+  const int32_t n = s->dd_n_send;
+  if (n > 0)
+    k_dd_pack<<<(unsigned)(((size_t)n * 56 + 255) / 256), 256, 0, s->stream>>>(s->K, s->d, n, s->dd_send_ids,
+                                                                              s->dd_step_dst);
+  k_dd_jumpers_rep<<<(s->K.N + 255) / 256, 256, 0, s->stream>>>(s->K, s->d, s->dd_step_S);
+  HIPCHK(s, hipGetLastError());
+  return KMC_OK;
+}
+
+int kmc_dd_step(kmc_sim* s, void* dst, double S, kmc_obs* out) {
+  if (!dd_ready(s)) return s ? fail(s, KMC_ERR_ARG, "dd: no decomposed state") : KMC_ERR_ARG;
+  s->dd_step_pending = true;
+  s->dd_step_dst = dst ? (unsigned char*)dst : s->dd_sendbuf;
+  s->dd_step_S = S;
+  const int rc = kmc_step(s, 1, out);
+  s->dd_step_pending = false;
+  return rc;
+}
+
+int kmc_dd_finish(kmc_sim* s, kmc_dd_report* out) {
   static_assert(sizeof(DDRep) == sizeof(kmc_dd_report), "kmc_dd_report layout");
   if (!out) return KMC_ERR_ARG;
   if (!dd_ready(s)) return s ? fail(s, KMC_ERR_ARG, "dd: no decomposed state") : KMC_ERR_ARG;
-  k_dd_jumpers_rep<<<(s->K.N + 255) / 256, 256, 0, s->stream>>>(s->K, s->d, S);
-  HIPCHK(s, hipGetLastError());
-  uint32_t xc[2];
   HIPCHK(s, hipMemcpyAsync(out, s->dd_rep, sizeof(DDRep), hipMemcpyDeviceToHost, s->stream));
-  HIPCHK(s, hipMemcpyAsync(xc, &s->d.ctl->dd_xcol, sizeof xc, hipMemcpyDeviceToHost, s->stream));
   // the step's counts and lists start again at zero (the entries are
   // overwritten before they are read)
-  HIPCHK(s, hipMemsetAsync(s->dd_rep, 0, offsetof(DDRep, jump_id), s->stream));
+  HIPCHK(s, hipMemsetAsync(&s->dd_rep->bad, 0, offsetof(DDRep, jump_id) - offsetof(DDRep, bad), s->stream));
   HIPCHK(s, hipStreamSynchronize(s->stream));
-  static_assert(offsetof(Ctl, dd_xbond) == offsetof(Ctl, dd_xcol) + sizeof(uint32_t), "Ctl dd counters");
-  out->xcol = xc[0];
-  out->xbond = xc[1];
   // a halo protein's bonds changed under the kept complexes: register them anew
   if (out->links) s->need_full = true;
   s->clusters_valid = false;

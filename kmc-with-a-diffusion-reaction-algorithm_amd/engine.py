@@ -87,7 +87,8 @@ def load_library(path: Optional[str] = None):
     L.kmc_dd_send_buffer.restype = C.c_void_p
     L.kmc_dd_send_buffer.argtypes = [C.c_void_p]
     L.kmc_dd_unpack.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32]
-    L.kmc_dd_finish.argtypes = [C.c_void_p, C.c_double, P(capi.DDReport)]
+    L.kmc_dd_finish.argtypes = [C.c_void_p, P(capi.DDReport)]
+    L.kmc_dd_step.argtypes = [C.c_void_p, C.c_void_p, C.c_double, C.c_void_p]
     L.kmc_dd_cut_count.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, P(C.c_int32)]
     L.kmc_list_growth.argtypes = [C.c_void_p]
     L.kmc_set_list_growth.argtypes = [C.c_void_p, C.c_int32]
@@ -361,9 +362,20 @@ class Simulation:
     def dd_unpack(self, src: int, first: int, n: int) -> None:
         self._check(load_library().kmc_dd_unpack(self._h, src, first, n))
 
-    def dd_finish(self, S: float) -> capi.DDReport:
+    def dd_step(self, dst: int, S: float) -> np.ndarray:
+        """One step of the window, its exchange rows packed into device
+        address dst (0: the handle's send buffer) and its jumpers beyond S
+        listed, in one wait; returns the step's record."""
+        out = np.zeros(1, dtype=capi.OBS_DTYPE)
+        self._check(load_library().kmc_dd_step(self._h, dst or None, S, out.ctypes.data_as(C.c_void_p)))
+        return out
+
+    def dd_send_address(self) -> int:
+        return int(load_library().kmc_dd_send_buffer(self._h) or 0)
+
+    def dd_finish(self) -> capi.DDReport:
         rep = capi.DDReport()
-        self._check(load_library().kmc_dd_finish(self._h, S, C.byref(rep)))
+        self._check(load_library().kmc_dd_finish(self._h, C.byref(rep)))
         return rep
 
     def dd_cut_count(self, ids: np.ndarray) -> int:

@@ -122,8 +122,12 @@ class LocalComm:
         self._bar.wait()
         return list(slots)
 
+    def send_address(self, me: "SlabRank") -> int:
+        return 0  # the window's own send buffer, which the others read in place
+
     def exchange(self, rank: int, me: "SlabRank") -> None:
-        ptr = me.eng.dd_pack() if me.eng_ok else None
+        """The rows were packed by the step (kmc_dd_step)."""
+        ptr = me.eng.dd_send_address() if me.eng_ok else None
         peers = self.allgather(rank, (ptr, me.send_first))
         if not me.eng_ok:
             return
@@ -165,19 +169,27 @@ class TorchComm:
             self._bufs[key] = b
         return b
 
-    def exchange(self, rank: int, me: "SlabRank") -> None:
+    def _edev(self, me: "SlabRank"):
         import torch
 
         dev = getattr(me.eng, "device", None)
         if self.device_backend and dev is None:
             raise SlabError("a device backend exchanges device buffers: the ranks' engines must be on GPUs")
-        edev = torch.device("cuda", dev) if dev is not None else torch.device("cpu")
+        return torch.device("cuda", dev) if dev is not None else torch.device("cpu")
+
+    def send_address(self, me: "SlabRank") -> int:
+        """The step packs its rows straight into the collective's send buffer."""
+        return self._buf("send", me.n_send * ROW, self._edev(me)).data_ptr()
+
+    def exchange(self, rank: int, me: "SlabRank") -> None:
+        """The rows were packed by the step (kmc_dd_step) into send_address()."""
+        import torch
+
+        edev = self._edev(me)
         wdev = edev if self.device_backend else torch.device("cpu")  # where the collective's buffers live
         ns, nr = me.n_send * ROW, me.n_recv * ROW
         send = self._buf("send", ns, edev)
-        if me.eng_ok:
-            me.eng.dd_pack(send.data_ptr())
-        else:
+        if not me.eng_ok:
             send.zero_()
         if wdev != edev:
             send = send[:ns].to(wdev)
@@ -697,7 +709,7 @@ class SlabRank:
         t0 = time.perf_counter()
         part, fail, err = None, False, None
         try:
-            part = self.eng.step(1)[0].copy()
+            part = self.eng.dd_step(self.comm.send_address(self), self.S - self.lead)[0].copy()
         except Exception as e:  # noqa: BLE001 — every rank must learn of it (the shares below)
             self.eng_ok = False
             if _engine_error(e) == capi.ERR_CAPACITY:
@@ -715,7 +727,7 @@ class SlabRank:
         dcol = dbond = 0
         xunits: Optional[list] = []
         if self.eng_ok:
-            rep = self.eng.dd_finish(self.S - self.lead)
+            rep = self.eng.dd_finish()
             t3 = time.perf_counter()
             sec["finish"] += t3 - t2
             bad = rep.bad
@@ -877,7 +889,8 @@ def _resorted(own_x: np.ndarray, xw: np.ndarray, moved: np.ndarray, owner: np.nd
             keep[j] = False
         out = out[keep]
     if gain.size:
-        out = np.sort(np.concatenate([out, xw[gain]]))
+        xg = np.sort(xw[gain])
+        out = np.insert(out, np.searchsorted(out, xg), xg)
     return out
 
 

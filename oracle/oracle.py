@@ -213,9 +213,18 @@ class Oracle:
     def dd_unpack(self, src: int, first: int, n: int) -> None:
         self._check(lib().oracle_dd_unpack(self.h, src, first, n))
 
-    def dd_finish(self, S: float):
+    def dd_step(self, dst: int, S: float):
+        out = Oracle.step(self, 1, want_hashes=False)[0]
+        self.dd_pack(dst)
+        self._dd_S = S  # the jumpers are listed at finish (the unpack leaves owned proteins alone)
+        return out
+
+    def dd_send_address(self) -> int:
+        return self._sendbuf.ctypes.data
+
+    def dd_finish(self):
         rep = capi.DDReport()
-        self._check(lib().oracle_dd_finish(self.h, S, C.byref(rep)))
+        self._check(lib().oracle_dd_finish(self.h, self._dd_S, C.byref(rep)))
         return rep
 
     def dd_cut_count(self, ids) -> int:
