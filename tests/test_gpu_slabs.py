@@ -98,7 +98,7 @@ def test_slabs_c3_steady_window():
         ref = sim.step(200).copy()
         ref_h = engine.state_hash(p, sim.get_state())
     assert int(st.counters[0]) > 50000
-    recs, ranks = slabs.run_local(p, st, 2, 200, window_handle, halo=1800.0, gather_every=200)
+    recs, ranks = slabs.run_local(p, st, 2, 200, window_handle, halo=2400.0, gather_every=200)
     s = ranks[0].stats
     h = engine.state_hash(p, ranks[0].last_global)
     for r in ranks:
