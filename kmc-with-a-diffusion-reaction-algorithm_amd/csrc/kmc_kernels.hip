@@ -2546,6 +2546,22 @@ __device__ __forceinline__ bool prefilter(bool mA, float mx, float my, float mzl
   return mA == qA ? same : mixed;  // branch-free: evaluated in the scans' inner loops
 }
 
+// The pair walk's filters with the xy differences on packed FP32
+// (v_pk_add_f32 / v_pk_mul_f32: two lanes of arithmetic per instruction; no
+// contraction, so every value is bit-identical to the scalar form): the
+// collision prefilter and the reaction prefilter share one dxy2.
+#ifndef PAIR_PK
+#define PAIR_PK 1
+#endif
+typedef float pk2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ bool prefilter_d(bool mA, float mzl, float mzh, bool qA, float4 r, float dxy2) {
+  const float dz = r.z - mzl;
+  const bool same = dxy2 + dz * dz < (mA ? 42.0f * 42.0f : 131.5f * 131.5f);
+  const float lz = mA ? r.z : mzl, alo = mA ? mzl : r.z, ahi = mA ? mzh : r.w;
+  const bool mixed = (dxy2 < 86.5f * 86.5f) & (lz > alo - 86.5f) & (lz < ahi + 86.5f);
+  return mA == qA ? same : mixed;
+}
+
 // ---------------------------------------------------------------- emitters
 // Output lists with one global counter: entries are staged in an LDS buffer
 // (slots handed out per wave: one LDS atomic per emitting wave-instruction),
@@ -3897,8 +3913,28 @@ __device__ __forceinline__ bool pair_scan_block(const KParams& P, const Dev& d, 
       [&](int il, int nl) {
         const int2 me = T.id[il], id = T.id[nl];
         const float4 mp = T.pos[il], rp = T.pos[nl];
+#if PAIR_PK
+        // col_pair and rxn_pair (below), one packed xy difference for both
+        const pk2 dd = (pk2){rp.x, rp.y} - (pk2){mp.x, mp.y};
+        const pk2 d2v = dd * dd;
+        const float dxy2 = d2v.x + d2v.y;
+        const int m = me.x & RID_PID, u = me.y, q = id.x & RID_PID, kq = id.y;
+        const bool isnew = id.x < 0, mA = !(me.x & RID_LIG), qB = (id.x & RID_LIG) != 0;
+        const bool own_ok = kq == u ? isnew : (kq > u ? !isnew : true);
+        const bool colp = (me.x < 0) & (u >= 0) & (q != m) & own_ok & prefilter_d(mA, mp.z, mp.w, !qB, rp, dxy2);
+        const float2 ms = site[il], qs = site[nl];
+        const pk2 tt = (pk2){qs.x, qs.y} - (pk2){ms.x, ms.y};
+        const pk2 t2v = tt * tt;
+        const bool rl_ok = qB & !(me.x & RID_ST2) & (dxy2 < 105.0f * 105.0f) & (rp.z > mp.z - 85.0f) &
+                           (rp.z < mp.w + 85.0f);
+        const float gap = fmaxf(fmaxf(rp.z - mp.w, mp.z - rp.w), 0.0f);
+        const bool cis_ok = !qB & !(me.x & RID_ST3) & !(id.x & RID_ST3) & (dxy2 < 57.0f * 57.0f) & (gap < 16.0f) &
+                            (t2v.x + t2v.y < 16.0f * 16.0f);
+        const bool rxp = rxn_item(me) & (q != m) & (rl_ok | cis_ok);
+#else
         const bool colp = me.x < 0 && me.y >= 0 && col_pair(me, mp, id, rp);
         const bool rxp = rxn_item(me) && rxn_pair(me, mp, site[il], id, rp, site[nl]);
+#endif
         push(colp, rxp, il, nl, id);
       });
   if (bad) atomicOr(&d.ctl->err, ERR_RESOLVE);
