@@ -1273,6 +1273,13 @@ int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out) {
                 "refined-out %u\n",
                 c[0], c[1], c[2], c[3], c[4], c[5], r[0], r[1], r[2], r[3], r[4]);
       }
+#if WALK_STATS
+      {
+        unsigned long long w = 0;
+        if (hipMemcpyFromSymbol(&w, HIP_SYMBOL(kmc_walk_pairs), sizeof w) == hipSuccess)
+          fprintf(stderr, "kmc walk pairs %llu (summed since the state was set)\n", w);
+      }
+#endif
       const uint64_t* t = s->ctl_host->stamps;
       if (t[16])
         fprintf(stderr, "kmc stamps heavy stage %llu align %llu writeback %llu records %llu (cycles summed over "

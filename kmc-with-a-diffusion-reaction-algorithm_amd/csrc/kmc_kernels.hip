@@ -3152,6 +3152,14 @@ __device__ __forceinline__ void item_ranges(const KParams& P, const TileLds& T, 
 #define WALK_MAXSEL 0    // profiles/r05/ab_walk/r7a_*: k_pair_scan 112.3 -> 113.0 us at C3, 1232 -> 1237 at C5)
 #endif
 #define PAIR_THREADS 256  // threads of a k_pair_scan workgroup (tile_walk's wave count)
+// -DWALK_STATS=1 (diagnostic build): the pairs the walks visit, summed over
+// the launch (read by KMC_DEBUG_COUNTS)
+#ifndef WALK_STATS
+#define WALK_STATS 0
+#endif
+#if WALK_STATS
+__device__ unsigned long long kmc_walk_pairs;
+#endif
 __device__ __forceinline__ int walk_item(int base, int lane, int wv, int nw) {
 #if WALK_PERM
   if (nw == 4) return base + 16 * ((5 * (lane >> 4) + 4 * wv) & 15) + (lane & 15);
@@ -3214,6 +3222,9 @@ __device__ __forceinline__ void tile_walk(const TileGeo& G, const TileLds& T, ui
       if (lane >= o) inc += t;
     }
     const int excl = inc - tot, wtot = __shfl(inc, 63, 64);
+#if WALK_STATS
+    if (lane == 0) atomicAdd(&kmc_walk_pairs, (unsigned long long)wtot);
+#endif
 #if !WALK_STRIDE
     const int l0 = l - lane;
 #endif
