@@ -105,3 +105,18 @@ def test_c5_regime_reaction_heavy_steady_state_window():
     for k in ("complex", "multi", "repeat", "reject", "rl", "mono", "cis", "rld", "md", "cd", "snap_bond",
               "snap_cis"):
         assert ev[k] > 0, k
+
+
+@pytest.mark.timeout(600)
+def test_c5_steady_state_step():
+    # C5 itself (1e7 particles, 1:1, 10x area density, reference physics) in a
+    # bond-rich state: 10 000 steps evolved on the GPU (≈ 750 000 bonds,
+    # multi-ligand complexes), then one step against the oracle, every field
+    # and the full-state hash (tools/c5_window.py runs the same check over 3
+    # steps after 2e4: profiles/r06/c5_window_r6i_final.log)
+    p = workloads.params("C5", seed=3)
+    ev, obs = _evolved_window(p, 10000, 1)
+    print("  C5 step events", ev, file=sys.stderr)
+    assert obs[-1]["bond_num"] > 100000
+    for k in ("complex", "multi", "reject", "snap_bond"):
+        assert ev[k] > 0, k
