@@ -125,6 +125,10 @@ class LocalComm:
     def send_address(self, me: "SlabRank") -> int:
         return 0  # the window's own send buffer, which the others read in place
 
+    def abort(self) -> None:
+        """A rank failed outside a collective: release the others' waits."""
+        self._bar.abort()
+
     def exchange(self, rank: int, me: "SlabRank") -> None:
         """The rows were packed by the step (kmc_dd_step)."""
         ptr = me.eng.dd_send_address() if me.eng_ok else None
@@ -159,6 +163,14 @@ class TorchComm:
         out = [None] * self.world
         self.dist.all_gather_object(out, obj)
         return out
+
+    def abort(self) -> None:
+        """A rank failed outside a collective: tear the group down, so that
+        the other ranks' next collective fails instead of waiting forever."""
+        try:
+            self.dist.destroy_process_group()
+        except Exception:  # noqa: BLE001 — already torn down or never complete
+            pass
 
     def _buf(self, key, nbytes, device):
         import torch
@@ -614,7 +626,17 @@ class SlabRank:
     # -- one step --------------------------------------------------------
     def step(self) -> np.ndarray:
         """Advance the trajectory one step; returns its bond.dat record (global,
-        a one-element capi.OBS_DTYPE array)."""
+        a one-element capi.OBS_DTYPE array).  An error on this rank that the
+        others cannot see (outside the per-step all-gather) aborts the comm."""
+        try:
+            return self._step()
+        except SlabError:
+            raise  # raised on every rank alike (from the all-gathered shares)
+        except BaseException:
+            self.comm.abort()
+            raise
+
+    def _step(self) -> np.ndarray:
         rec = self._one()
         tries = 0
         while rec is None:  # a check failed on some slab: back to the step before, re-partition, retry

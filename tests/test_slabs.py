@@ -10,6 +10,7 @@ different slabs collide and bond across the cut.
 """
 import os
 import socket
+import time
 
 import numpy as np
 import pytest
@@ -212,3 +213,46 @@ def test_slab_fixture_pinned():
     obs, hashes = o.step(30)
     assert np.array_equal(obs, fx["obs"][:30]) and np.array_equal(hashes, fx["hashes"][:30])
     assert int(fx["obs"][-1]["bond_num"]) > 0
+
+
+def _failing_worker(rank, world, port):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    p, st = scenario(2000, 700, 4500.0, seed=23)
+    me = slabs.SlabRank(p, rank, slabs.TorchComm(), OracleWindow)
+    me.start(st)
+    if rank == 1:  # an error only this rank sees, between two collectives
+        orig = me._jumper_check
+
+        def boom(ids, xs):
+            if me.step_no >= 4:
+                raise RuntimeError("injected failure on rank 1")
+            return orig(ids, xs)
+
+        me._jumper_check = boom
+    try:
+        for _ in range(20):
+            me.step()
+    except RuntimeError:
+        if rank == 1:
+            # the failing rank stays alive (a driver writing its logs, say):
+            # only the torn-down process group can release the other rank
+            time.sleep(60)
+        raise
+
+
+def test_slabs_one_rank_failure_ends_every_rank():
+    # an error raised on one rank only must not leave the others
+    # waiting in their next collective forever — the failing rank tears the
+    # process group down, and the other rank's collective fails at once
+    ctx = mp.spawn(_failing_worker, args=(2, _free_port()), nprocs=2, join=False)
+    ctx.processes[0].join(timeout=40)
+    waiting = ctx.processes[0].is_alive()
+    for proc in ctx.processes:
+        if proc.is_alive():
+            proc.kill()
+        proc.join()
+    assert not waiting, "rank 0 still waits in a collective after rank 1 failed"
+    assert ctx.processes[0].exitcode != 0
