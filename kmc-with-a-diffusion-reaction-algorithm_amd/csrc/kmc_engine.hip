@@ -28,6 +28,9 @@ static const char* const KNAMES[KI_N] = {
     "k_pair_scan", "k_col_exact", "k_col_rounds", "k_commit_rxn",
     "k_match", "k_diss_observe", "slot_resort"};
 #define TRING 64  // steps of event pairs kept in flight
+#ifndef CX_STREAM_DEFAULT  // the complex chain on its own stream unless KMC_CX_STREAM=0 (1) / only with =1 (0)
+#define CX_STREAM_DEFAULT 0
+#endif
 
 struct kmc_sim {
   kmc_params p;
@@ -96,6 +99,12 @@ struct kmc_sim {
   // arguments are byte-identical, so the graphs cycle with the buffer parity
   static constexpr int NGRAPH = 4;
   bool use_graphs = false;
+  // the complex chain (their rigid-move parameters, k_move_members,
+  // k_cx_check, k_complex_heavy) on a second stream beside the free units'
+  // proposals (KMC_CX_STREAM; forked after k_bfs, joined before the pair scan)
+  bool cx_stream = false;
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   struct StepGraph {
     bool valid = false;
     unsigned char key[sizeof(KParams) + sizeof(Dev)];
@@ -448,6 +457,8 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
     K.cx_serial = cxs && *cxs == '1';
     const char* gr = getenv("KMC_GRAPH");
     s->use_graphs = gr && *gr == '1';
+    const char* cs = getenv("KMC_CX_STREAM");
+    s->cx_stream = CX_STREAM_DEFAULT ? !(cs && *cs == '0') : (cs && *cs == '1');
     const char* ht = getenv("KMC_DEBUG_HTAG");  // debug: fewer tagged home entries (the searched lookup)
     K.htag_max = HTAG_MAX;
     if (ht && *ht) K.htag_max = std::max(0, std::min(HTAG_MAX, atoi(ht)));
@@ -496,6 +507,10 @@ int kmc_destroy(kmc_sim* s) {
     if (e) (void)hipEventDestroy(e);
   for (auto& g : s->graphs)
     if (g.exec) (void)hipGraphExecDestroy(g.exec);
+  if (s->side) (void)hipStreamSynchronize(s->side);
+  if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);
+  if (s->ev_join) (void)hipEventDestroy(s->ev_join);
+  if (s->side) (void)hipStreamDestroy(s->side);
   if (s->stream) (void)hipStreamDestroy(s->stream);
   delete s;
   return KMC_OK;
@@ -898,14 +913,15 @@ struct Bracket {
     }
   }
 };
-#define TIMED(k, ...)                                                                                   \
+#define TIMED(k, ...) TIMED_ON(k, s->stream, __VA_ARGS__)
+#define TIMED_ON(k, STREAM, ...)                                                                        \
   do {                                                                                                  \
     {                                                                                                   \
-      Bracket b_(s, k, s->stream);                                                                      \
+      Bracket b_(s, k, STREAM);                                                                         \
       __VA_ARGS__;                                                                                      \
     }                                                                                                   \
     if (s->debug_sync) {                                                                                \
-      const hipError_t e_ = hipStreamSynchronize(s->stream);                                            \
+      const hipError_t e_ = hipStreamSynchronize(STREAM);                                               \
       if (e_ != hipSuccess)                                                                             \
         return fail(s, KMC_ERR_HIP, std::string("KMC_DEBUG_SYNC: ") + KNAMES[k] + " failed in step " +     \
                                         std::to_string(s->launch_base) + ": " + hipGetErrorString(e_)); \
@@ -994,11 +1010,33 @@ static int launch_step(kmc_sim* s, bool re_sort) {
       TIMED(KI_BFS, (k_bfs<<<gB, T, 0, st>>>(K, d)));
     }
     const int gC = K.NB > 0 ? std::min(gL, 512) : 0;  // grid-stride over the descriptor list
-    TIMED(KI_PROPOSE_FREE, (k_propose_free<<<gC + gN, T, 0, st>>>(K, d, gC)));
-    if (K.NB > 0) {
-      TIMED(KI_MOVE_MEMBERS, (k_move_members<<<gN, T, 0, st>>>(K, d)));
-      TIMED(KI_CX_CHECK, (k_cx_check<<<gL, T, 0, st>>>(K, d)));
-      TIMED(KI_CX_HEAVY, (k_complex_heavy<<<1024, T, 0, st>>>(K, d)));
+    if (s->cx_stream && K.NB > 0 && !s->use_graphs) {
+      // the complex chain beside the free units (disjoint slots, records and
+      // beads; shared lists only through atomics): the free units stream HBM
+      // while the complexes' dependent chains wait on latency
+      if (!s->side) {
+        if (hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming) != hipSuccess)
+          return fail(s, KMC_ERR_HIP, "the complexes' stream");
+      }
+      hipStream_t sd = s->side;
+      HIPCHK(s, hipEventRecord(s->ev_fork, st));
+      HIPCHK(s, hipStreamWaitEvent(sd, s->ev_fork, 0));
+      k_propose_free<<<gC, T, 0, sd>>>(K, d, gC);  // cx_params only (the bracket of the id is the free units')
+      TIMED_ON(KI_MOVE_MEMBERS, sd, (k_move_members<<<gN, T, 0, sd>>>(K, d)));
+      TIMED_ON(KI_CX_CHECK, sd, (k_cx_check<<<gL, T, 0, sd>>>(K, d)));
+      TIMED_ON(KI_CX_HEAVY, sd, (k_complex_heavy<<<1024, T, 0, sd>>>(K, d)));
+      HIPCHK(s, hipEventRecord(s->ev_join, sd));
+      TIMED(KI_PROPOSE_FREE, (k_propose_free<<<gN, T, 0, st>>>(K, d, 0)));  // the free units
+      HIPCHK(s, hipStreamWaitEvent(st, s->ev_join, 0));
+    } else {
+      TIMED(KI_PROPOSE_FREE, (k_propose_free<<<gC + gN, T, 0, st>>>(K, d, gC)));
+      if (K.NB > 0) {
+        TIMED(KI_MOVE_MEMBERS, (k_move_members<<<gN, T, 0, st>>>(K, d)));
+        TIMED(KI_CX_CHECK, (k_cx_check<<<gL, T, 0, st>>>(K, d)));
+        TIMED(KI_CX_HEAVY, (k_complex_heavy<<<1024, T, 0, st>>>(K, d)));
+      }
     }
   }
   if (K.dbg_recs) k_rec_check<<<std::min(2048, (2 * K.N + T - 1) / T), T, 0, st>>>(K, d);
