@@ -1006,14 +1006,17 @@ static int launch_step(kmc_sim* s, bool re_sort) {
   {
     Bracket b_(s, KI_PROPOSE, st);
     const int gL = std::min(2048, (K.NB + T - 1) / T);  // grid-stride over the descriptor list
-    if (K.NB > 0) {
+    const bool side = s->cx_stream && K.NB > 0 && !s->use_graphs;
+    if (K.NB > 0 && !side) {
       TIMED(KI_BFS, (k_bfs<<<gB, T, 0, st>>>(K, d)));
     }
     const int gC = K.NB > 0 ? std::min(gL, 512) : 0;  // grid-stride over the descriptor list
-    if (s->cx_stream && K.NB > 0 && !s->use_graphs) {
-      // the complex chain beside the free units (disjoint slots, records and
-      // beads; shared lists only through atomics): the free units stream HBM
-      // while the complexes' dependent chains wait on latency
+    if (side) {
+      // the complex chain — BFS of the candidates, rigid-move parameters,
+      // members, checks, heavy path — beside the free units (k_classify has
+      // settled every free unit; disjoint slots, records and beads; shared
+      // lists only through atomics): the free units stream HBM while the
+      // complexes' dependent chains wait on latency
       if (!s->side) {
         if (hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming) != hipSuccess ||
@@ -1023,6 +1026,7 @@ static int launch_step(kmc_sim* s, bool re_sort) {
       hipStream_t sd = s->side;
       HIPCHK(s, hipEventRecord(s->ev_fork, st));
       HIPCHK(s, hipStreamWaitEvent(sd, s->ev_fork, 0));
+      TIMED_ON(KI_BFS, sd, (k_bfs<<<gB, T, 0, sd>>>(K, d)));
       k_propose_free<<<gC, T, 0, sd>>>(K, d, gC);  // cx_params only (the bracket of the id is the free units')
       TIMED_ON(KI_MOVE_MEMBERS, sd, (k_move_members<<<gN, T, 0, sd>>>(K, d)));
       TIMED_ON(KI_CX_CHECK, sd, (k_cx_check<<<gL, T, 0, sd>>>(K, d)));
