@@ -1317,9 +1317,10 @@ int kmc_step(kmc_sim* s, int64_t nsteps, kmc_obs* out) {
       }
 #if WALK_STATS
       {
-        unsigned long long w = 0;
-        if (hipMemcpyFromSymbol(&w, HIP_SYMBOL(kmc_walk_pairs), sizeof w) == hipSuccess)
-          fprintf(stderr, "kmc walk pairs %llu (summed since the state was set)\n", w);
+        unsigned long long w = 0, wo = 0;
+        if (hipMemcpyFromSymbol(&w, HIP_SYMBOL(kmc_walk_pairs), sizeof w) == hipSuccess &&
+            hipMemcpyFromSymbol(&wo, HIP_SYMBOL(kmc_walk_pairs_old), sizeof wo) == hipSuccess)
+          fprintf(stderr, "kmc walk pairs %llu old-position items %llu (summed since the library loaded)\n", w, wo);
       }
 #endif
       const uint64_t* t = s->ctl_host->stamps;

@@ -3159,6 +3159,7 @@ __device__ __forceinline__ void item_ranges(const KParams& P, const TileLds& T, 
 #endif
 #if WALK_STATS
 __device__ unsigned long long kmc_walk_pairs;
+__device__ unsigned long long kmc_walk_pairs_old;  // of them, the pairs of old-position (non-proposal) items
 #endif
 __device__ __forceinline__ int walk_item(int base, int lane, int wv, int nw) {
 #if WALK_PERM
@@ -3224,6 +3225,13 @@ __device__ __forceinline__ void tile_walk(const TileGeo& G, const TileLds& T, ui
     const int excl = inc - tot, wtot = __shfl(inc, 63, 64);
 #if WALK_STATS
     if (lane == 0) atomicAdd(&kmc_walk_pairs, (unsigned long long)wtot);
+    {
+      int old = (item && T.id[l].x >= 0) ? r1[0] - r0[0] + r1[1] - r0[1] + r1[2] - r0[2] + r1[3] - r0[3] +
+                                               r1[4] - r0[4] + r1[5] - r0[5]
+                                         : 0;
+      for (int o = 32; o > 0; o >>= 1) old += __shfl_down(old, o, 64);
+      if (lane == 0) atomicAdd(&kmc_walk_pairs_old, (unsigned long long)old);
+    }
 #endif
 #if !WALK_STRIDE
     const int l0 = l - lane;
