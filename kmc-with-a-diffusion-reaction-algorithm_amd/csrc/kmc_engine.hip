@@ -28,8 +28,8 @@ static const char* const KNAMES[KI_N] = {
     "k_pair_scan", "k_col_exact", "k_col_rounds", "k_commit_rxn",
     "k_match", "k_diss_observe", "slot_resort"};
 #define TRING 64  // steps of event pairs kept in flight
-#ifndef CX_STREAM_DEFAULT  // the complex chain on its own stream unless KMC_CX_STREAM=0 (1) / only with =1 (0)
-#define CX_STREAM_DEFAULT 0
+#ifndef CX_STREAM_N  // proteins from which the complex chain runs on its own stream (kmc_create)
+#define CX_STREAM_N (4 << 20)
 #endif
 
 struct kmc_sim {
@@ -457,8 +457,12 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
     K.cx_serial = cxs && *cxs == '1';
     const char* gr = getenv("KMC_GRAPH");
     s->use_graphs = gr && *gr == '1';
+    // the complex chain on a second stream from CX_STREAM_N proteins (C5: 4.043
+    // -> 3.987 ms/step; C3: 0.457 -> 0.466, the free units slowed by the
+    // contention more than the chain hides: profiles/r06/ab_cx_stream_*);
+    // KMC_CX_STREAM=0 / 1 forces it
     const char* cs = getenv("KMC_CX_STREAM");
-    s->cx_stream = CX_STREAM_DEFAULT ? !(cs && *cs == '0') : (cs && *cs == '1');
+    s->cx_stream = (cs && *cs) ? *cs == '1' : (int64_t)N >= CX_STREAM_N;
     const char* ht = getenv("KMC_DEBUG_HTAG");  // debug: fewer tagged home entries (the searched lookup)
     K.htag_max = HTAG_MAX;
     if (ht && *ht) K.htag_max = std::max(0, std::min(HTAG_MAX, atoi(ht)));
