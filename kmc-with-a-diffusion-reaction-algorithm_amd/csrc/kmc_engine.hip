@@ -102,7 +102,7 @@ struct kmc_sim {
   // the complex chain (their rigid-move parameters, k_move_members,
   // k_cx_check, k_complex_heavy) on a second stream beside the free units'
   // proposals (KMC_CX_STREAM; forked after k_bfs, joined before the pair scan)
-  bool cx_stream = false;
+  int cx_stream = 0;  // 1: the whole chain on the side stream; 2: only k_bfs and the parameters
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   struct StepGraph {
@@ -462,7 +462,7 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
     // contention more than the chain hides: profiles/r06/ab_cx_stream_*);
     // KMC_CX_STREAM=0 / 1 forces it
     const char* cs = getenv("KMC_CX_STREAM");
-    s->cx_stream = (cs && *cs) ? *cs == '1' : (int64_t)N >= CX_STREAM_N;
+    s->cx_stream = (cs && *cs) ? std::max(0, std::min(2, atoi(cs))) : ((int64_t)N >= CX_STREAM_N ? 1 : 0);
     const char* ht = getenv("KMC_DEBUG_HTAG");  // debug: fewer tagged home entries (the searched lookup)
     K.htag_max = HTAG_MAX;
     if (ht && *ht) K.htag_max = std::max(0, std::min(HTAG_MAX, atoi(ht)));
@@ -1010,7 +1010,7 @@ static int launch_step(kmc_sim* s, bool re_sort) {
   {
     Bracket b_(s, KI_PROPOSE, st);
     const int gL = std::min(2048, (K.NB + T - 1) / T);  // grid-stride over the descriptor list
-    const bool side = s->cx_stream && K.NB > 0 && !s->use_graphs;
+    const bool side = s->cx_stream != 0 && K.NB > 0 && !s->use_graphs;
     if (K.NB > 0 && !side) {
       TIMED(KI_BFS, (k_bfs<<<gB, T, 0, st>>>(K, d)));
     }
@@ -1032,12 +1032,19 @@ static int launch_step(kmc_sim* s, bool re_sort) {
       HIPCHK(s, hipStreamWaitEvent(sd, s->ev_fork, 0));
       TIMED_ON(KI_BFS, sd, (k_bfs<<<gB, T, 0, sd>>>(K, d)));
       k_propose_free<<<gC, T, 0, sd>>>(K, d, gC);  // cx_params only (the bracket of the id is the free units')
-      TIMED_ON(KI_MOVE_MEMBERS, sd, (k_move_members<<<gN, T, 0, sd>>>(K, d)));
-      TIMED_ON(KI_CX_CHECK, sd, (k_cx_check<<<gL, T, 0, sd>>>(K, d)));
-      TIMED_ON(KI_CX_HEAVY, sd, (k_complex_heavy<<<1024, T, 0, sd>>>(K, d)));
+      if (s->cx_stream == 1) {
+        TIMED_ON(KI_MOVE_MEMBERS, sd, (k_move_members<<<gN, T, 0, sd>>>(K, d)));
+        TIMED_ON(KI_CX_CHECK, sd, (k_cx_check<<<gL, T, 0, sd>>>(K, d)));
+        TIMED_ON(KI_CX_HEAVY, sd, (k_complex_heavy<<<1024, T, 0, sd>>>(K, d)));
+      }
       HIPCHK(s, hipEventRecord(s->ev_join, sd));
       TIMED(KI_PROPOSE_FREE, (k_propose_free<<<gN, T, 0, st>>>(K, d, 0)));  // the free units
       HIPCHK(s, hipStreamWaitEvent(st, s->ev_join, 0));
+      if (s->cx_stream == 2) {  // the members' streams after the free units', on the main stream
+        TIMED(KI_MOVE_MEMBERS, (k_move_members<<<gN, T, 0, st>>>(K, d)));
+        TIMED(KI_CX_CHECK, (k_cx_check<<<gL, T, 0, st>>>(K, d)));
+        TIMED(KI_CX_HEAVY, (k_complex_heavy<<<1024, T, 0, st>>>(K, d)));
+      }
     } else {
       TIMED(KI_PROPOSE_FREE, (k_propose_free<<<gC + gN, T, 0, st>>>(K, d, gC)));
       if (K.NB > 0) {
