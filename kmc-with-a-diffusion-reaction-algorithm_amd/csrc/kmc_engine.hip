@@ -1022,7 +1022,15 @@ static int launch_step(kmc_sim* s, bool re_sort) {
       // lists only through atomics): the free units stream HBM while the
       // complexes' dependent chains wait on latency
       if (!s->side) {
-        if (hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking) != hipSuccess ||
+        // the chain is the longer path (its kernels wait on latency; starved
+        // of workgroup slots by the free units' stream they ran 2-5x slower):
+        // its stream gets the device's highest priority unless
+        // KMC_CX_STREAM_PRIO=0
+        int lo = 0, hi = 0;
+        const char* pr = getenv("KMC_CX_STREAM_PRIO");
+        const bool prio = !(pr && *pr == '0') && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess;
+        if ((prio ? hipStreamCreateWithPriority(&s->side, hipStreamNonBlocking, hi)
+                  : hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking)) != hipSuccess ||
             hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming) != hipSuccess)
           return fail(s, KMC_ERR_HIP, "the complexes' stream");
