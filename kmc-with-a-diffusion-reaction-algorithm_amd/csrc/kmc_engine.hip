@@ -102,7 +102,8 @@ struct kmc_sim {
   // the complex chain (their rigid-move parameters, k_move_members,
   // k_cx_check, k_complex_heavy) on a second stream beside the free units'
   // proposals (KMC_CX_STREAM; forked after k_bfs, joined before the pair scan)
-  int cx_stream = 0;  // 1: the whole chain on the side stream; 2: only k_bfs and the parameters
+  int cx_stream = 0;  // 1: the whole chain on the side stream; 2: only k_bfs and the parameters;
+                      // 3: k_cx_check and k_complex_heavy beside the free units (after the members)
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   struct StepGraph {
@@ -457,12 +458,13 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
     K.cx_serial = cxs && *cxs == '1';
     const char* gr = getenv("KMC_GRAPH");
     s->use_graphs = gr && *gr == '1';
-    // the complex chain on a second stream from CX_STREAM_N proteins (C5: 4.043
-    // -> 3.987 ms/step; C3: 0.457 -> 0.466, the free units slowed by the
-    // contention more than the chain hides: profiles/r06/ab_cx_stream_*);
-    // KMC_CX_STREAM=0 / 1 forces it
+    // the complexes' checks and heavy path on a second stream beside the free
+    // units from CX_STREAM_N proteins (mode 3; C5: 3.90 (none) / 3.85 (the
+    // whole chain beside them, mode 1) -> 3.67 ms/step; C3: 0.452 / 0.455 /
+    // 0.468, the latency chains slowed by the free units' HBM stream more
+    // than they hide: profiles/r06/ab_cx_stream3_*); KMC_CX_STREAM=0..3 forces a mode
     const char* cs = getenv("KMC_CX_STREAM");
-    s->cx_stream = (cs && *cs) ? std::max(0, std::min(2, atoi(cs))) : ((int64_t)N >= CX_STREAM_N ? 1 : 0);
+    s->cx_stream = (cs && *cs) ? std::max(0, std::min(3, atoi(cs))) : ((int64_t)N >= CX_STREAM_N ? 3 : 0);
     const char* ht = getenv("KMC_DEBUG_HTAG");  // debug: fewer tagged home entries (the searched lookup)
     K.htag_max = HTAG_MAX;
     if (ht && *ht) K.htag_max = std::max(0, std::min(HTAG_MAX, atoi(ht)));
@@ -971,6 +973,23 @@ static int debug_check_lists(kmc_sim* s) {
 #define COARSE_N (4 << 20)
 #endif
 // s->tnow (this step bracketed) is set by the caller
+// the complexes' stream and its fork / join events, made on first use
+static int side_stream(kmc_sim* s) {
+  if (s->side) return KMC_OK;
+  // the chain is the longer path (its kernels wait on latency; starved of
+  // workgroup slots by the free units' stream they ran 2-5x slower): its
+  // stream gets the device's highest priority unless KMC_CX_STREAM_PRIO=0
+  int lo = 0, hi = 0;
+  const char* pr = getenv("KMC_CX_STREAM_PRIO");
+  const bool prio = !(pr && *pr == '0') && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess;
+  if ((prio ? hipStreamCreateWithPriority(&s->side, hipStreamNonBlocking, hi)
+            : hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking)) != hipSuccess ||
+      hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming) != hipSuccess)
+    return fail(s, KMC_ERR_HIP, "the complexes' stream");
+  return KMC_OK;
+}
+
 static int launch_step(kmc_sim* s, bool re_sort) {
   const KParams& K = s->K;
   Dev& d = s->d;
@@ -1011,30 +1030,34 @@ static int launch_step(kmc_sim* s, bool re_sort) {
     Bracket b_(s, KI_PROPOSE, st);
     const int gL = std::min(2048, (K.NB + T - 1) / T);  // grid-stride over the descriptor list
     const bool side = s->cx_stream != 0 && K.NB > 0 && !s->use_graphs;
-    if (K.NB > 0 && !side) {
+    if (K.NB > 0 && (!side || s->cx_stream == 3)) {
       TIMED(KI_BFS, (k_bfs<<<gB, T, 0, st>>>(K, d)));
     }
     const int gC = K.NB > 0 ? std::min(gL, 512) : 0;  // grid-stride over the descriptor list
-    if (side) {
+    if (side && s->cx_stream == 3) {
+      // the members' HBM stream first, alone; then the complexes' checks and
+      // heavy path (dependent chains waiting on latency) beside the free
+      // units' HBM stream
+      const int rc = side_stream(s);
+      if (rc != KMC_OK) return rc;
+      hipStream_t sd = s->side;
+      k_propose_free<<<gC, T, 0, st>>>(K, d, gC);  // cx_params only
+      TIMED(KI_MOVE_MEMBERS, (k_move_members<<<gN, T, 0, st>>>(K, d)));
+      HIPCHK(s, hipEventRecord(s->ev_fork, st));
+      HIPCHK(s, hipStreamWaitEvent(sd, s->ev_fork, 0));
+      TIMED_ON(KI_CX_CHECK, sd, (k_cx_check<<<gL, T, 0, sd>>>(K, d)));
+      TIMED_ON(KI_CX_HEAVY, sd, (k_complex_heavy<<<1024, T, 0, sd>>>(K, d)));
+      HIPCHK(s, hipEventRecord(s->ev_join, sd));
+      TIMED(KI_PROPOSE_FREE, (k_propose_free<<<gN, T, 0, st>>>(K, d, 0)));  // the free units
+      HIPCHK(s, hipStreamWaitEvent(st, s->ev_join, 0));
+    } else if (side) {
       // the complex chain — BFS of the candidates, rigid-move parameters,
       // members, checks, heavy path — beside the free units (k_classify has
       // settled every free unit; disjoint slots, records and beads; shared
       // lists only through atomics): the free units stream HBM while the
       // complexes' dependent chains wait on latency
-      if (!s->side) {
-        // the chain is the longer path (its kernels wait on latency; starved
-        // of workgroup slots by the free units' stream they ran 2-5x slower):
-        // its stream gets the device's highest priority unless
-        // KMC_CX_STREAM_PRIO=0
-        int lo = 0, hi = 0;
-        const char* pr = getenv("KMC_CX_STREAM_PRIO");
-        const bool prio = !(pr && *pr == '0') && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess;
-        if ((prio ? hipStreamCreateWithPriority(&s->side, hipStreamNonBlocking, hi)
-                  : hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking)) != hipSuccess ||
-            hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming) != hipSuccess)
-          return fail(s, KMC_ERR_HIP, "the complexes' stream");
-      }
+      const int rc = side_stream(s);
+      if (rc != KMC_OK) return rc;
       hipStream_t sd = s->side;
       HIPCHK(s, hipEventRecord(s->ev_fork, st));
       HIPCHK(s, hipStreamWaitEvent(sd, s->ev_fork, 0));
