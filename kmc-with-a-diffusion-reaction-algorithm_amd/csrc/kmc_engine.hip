@@ -106,6 +106,7 @@ struct kmc_sim {
                       // 3: k_cx_check and k_complex_heavy beside the free units (after the members)
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  int cx_params_wg = 0;  // mode 3: workgroups of the parameters' launch (KMC_CX_PARAMS_WG; 0: gL)
   struct StepGraph {
     bool valid = false;
     unsigned char key[sizeof(KParams) + sizeof(Dev)];
@@ -465,6 +466,8 @@ int kmc_create(const kmc_params* p, int device, kmc_sim** out) {
     // than they hide: profiles/r06/ab_cx_stream3_*); KMC_CX_STREAM=0..3 forces a mode
     const char* cs = getenv("KMC_CX_STREAM");
     s->cx_stream = (cs && *cs) ? std::max(0, std::min(3, atoi(cs))) : ((int64_t)N >= CX_STREAM_N ? 3 : 0);
+    const char* cpw = getenv("KMC_CX_PARAMS_WG");
+    s->cx_params_wg = cpw && *cpw ? std::max(0, atoi(cpw)) : 0;
     const char* ht = getenv("KMC_DEBUG_HTAG");  // debug: fewer tagged home entries (the searched lookup)
     K.htag_max = HTAG_MAX;
     if (ht && *ht) K.htag_max = std::max(0, std::min(HTAG_MAX, atoi(ht)));
@@ -1034,6 +1037,7 @@ static int launch_step(kmc_sim* s, bool re_sort) {
       TIMED(KI_BFS, (k_bfs<<<gB, T, 0, st>>>(K, d)));
     }
     const int gC = K.NB > 0 ? std::min(gL, 512) : 0;  // grid-stride over the descriptor list
+    const int gP3 = s->cx_params_wg > 0 ? std::min(s->cx_params_wg, 1 << 16) : gL;
     if (side && s->cx_stream == 3) {
       // the members' HBM stream first, alone; then the complexes' checks and
       // heavy path (dependent chains waiting on latency) beside the free
@@ -1041,7 +1045,9 @@ static int launch_step(kmc_sim* s, bool re_sort) {
       const int rc = side_stream(s);
       if (rc != KMC_OK) return rc;
       hipStream_t sd = s->side;
-      k_propose_free<<<gC, T, 0, st>>>(K, d, gC);  // cx_params only
+      // cx_params only, alone: one thread per complex up to gL workgroups (its
+      // chains of loads and fdlibm calls hidden by occupancy, not by a stream)
+      k_propose_free<<<gP3, T, 0, st>>>(K, d, gP3);
       TIMED(KI_MOVE_MEMBERS, (k_move_members<<<gN, T, 0, st>>>(K, d)));
       HIPCHK(s, hipEventRecord(s->ev_fork, st));
       HIPCHK(s, hipStreamWaitEvent(sd, s->ev_fork, 0));
