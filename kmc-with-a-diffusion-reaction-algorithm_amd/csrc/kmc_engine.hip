@@ -1045,8 +1045,8 @@ static int launch_step(kmc_sim* s, bool re_sort) {
       const int rc = side_stream(s);
       if (rc != KMC_OK) return rc;
       hipStream_t sd = s->side;
-      // cx_params only, alone: one thread per complex up to gL workgroups (its
-      // chains of loads and fdlibm calls hidden by occupancy, not by a stream)
+      // cx_params only, alone (one thread per complex up to gL workgroups;
+      // 512 / gL / 4 096 workgroups: equal at C5, 128 us, profiles/r06/ab_cx_params_wg_C5)
       k_propose_free<<<gP3, T, 0, st>>>(K, d, gP3);
       TIMED(KI_MOVE_MEMBERS, (k_move_members<<<gN, T, 0, st>>>(K, d)));
       HIPCHK(s, hipEventRecord(s->ev_fork, st));
