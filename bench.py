@@ -70,6 +70,12 @@ def kernel_bytes(name: str, n_a: int, n_b: int):
 
 
 TRAFFIC_JSON = "profiles/traffic_C3.json"
+# wave64 VALU instructions per launch (SQ_INSTS_VALU) from the committed SQ
+# pass of the same steady-state profile (profiles/r06/final_C3/pmc_summary.txt)
+VALU_JSON = "profiles/valu_C3.json"
+# VALU issue ceiling: 256 CUs × 4 SIMDs, one wave64 instruction per SIMD every
+# 4 cycles (16 lanes wide) at 2.4 GHz (MI355X_MICROARCH.md: max clock)
+VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 4
 
 
 # the proposal phase the engine brackets as "k_propose" (kmc_engine.hip
@@ -95,6 +101,15 @@ def pmc_traffic(kernel: str, workload: str):
     names = PROPOSE_PHASE if kernel == "k_propose" else (kernel_trace_name(kernel),)
     recs = [t.get(n) for n in names]
     return sum(r["traffic_bytes"] for r in recs) if all(recs) else None
+
+
+def pmc_valu(kernel: str, workload: str):
+    """SQ_INSTS_VALU per launch of `kernel` from VALU_JSON (C3 only), or None."""
+    path = os.path.join(REPO, VALU_JSON)
+    if workload != "C3" or not os.path.exists(path):
+        return None
+    r = json.load(open(path)).get(kernel_trace_name(kernel))
+    return r["SQ_INSTS_VALU"] if r else None
 
 
 def kernel_trace_name(name: str) -> str:
@@ -366,6 +381,12 @@ def run_rank(args, rank: int, world: int, local: int):
             "achieved_by_traffic": (tr_k / a_s / 1e9) if tr_k else None,
             "frac_by_traffic": (tr_k / a_s / 1e9 / HBM_PEAK_GBS) if tr_k else None,
         }
+        valu = pmc_valu(k, args.workload)
+        if valu:
+            # the issue-bound view (the pair walk: VALU-issue-bound, not HBM)
+            detail[k]["valu_per_launch"] = valu
+            detail[k]["valu_issue_ms"] = valu / VALU_ISSUE_PEAK * 1e3
+            detail[k]["frac_of_valu_issue"] = valu / VALU_ISSUE_PEAK / a_s
     kb = kernel_bytes(dom, p.n_a, p.n_b)
     achieved = (kb / avg_s / 1e9) if (kb and avg_s > 0) else None
     traffic = pmc_traffic(dom, args.workload)
